@@ -1,0 +1,181 @@
+/*
+ * mpiasyncpools.h — C ABI of the MI355X-native `asyncmap!` hot path of MPIAsyncPools.jl
+ * (severinson/MPIStragglers.jl, package `MPIAsyncPools` v0.1.0).
+ *
+ * Plain C: opaque handles, raw pointers, byte sizes, int status codes.  No torch or HIP
+ * types appear in any signature (streams are passed as `void*` = hipStream_t).
+ *
+ * Reference interface each entry point replaces (file:line in the reference tree):
+ *
+ *   mpa_pool_create / mpa_pool_destroy
+ *       MPIAsyncPool(ranks; epoch0, nwait)            src/MPIAsyncPools.jl:35-43
+ *       MPIAsyncPool(n)                               src/MPIAsyncPools.jl:46
+ *   mpa_pool_ranks / _sepochs / _repochs / _active / _stimestamps / _latency /
+ *   mpa_pool_nwait / mpa_pool_epoch   (borrowed, aliasing the pool's state)
+ *       the MPIAsyncPool fields                       src/MPIAsyncPools.jl:25-34
+ *   mpa_asyncmap
+ *       Base.asyncmap!(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm;
+ *                      nwait, epoch, tag) -> repochs  src/MPIAsyncPools.jl:68-188
+ *   mpa_waitall
+ *       waitall!(pool, recvbuf, irecvbuf) -> repochs  src/MPIAsyncPools.jl:195-224
+ *   mpa_comm_*
+ *       the `comm::MPI.Comm` argument (MPI.COMM_WORLD, examples/iterative_example.jl:8)
+ *       together with the worker programs that answer on it (worker_main,
+ *       examples/iterative_example.jl:55-82, test/kmap1.jl:23-33,
+ *       test/kmap2.jl:110-132): a communicator whose ranks 1..n are device workers,
+ *       each running a registered task on its own HIP stream.
+ *   mpa_comm_shutdown
+ *       the control-tag shutdown (examples/iterative_example.jl:49-52,
+ *       test/kmap2.jl:48-52)
+ *   mpa_aggregate / mpa_lsq_update
+ *       the coordinator's consumption of `recvbuf` chunks
+ *       (examples/iterative_example.jl:41-46, test/kmap2.jl:71-85) as device kernels.
+ *
+ * Status codes map onto the reference's exceptions: MPA_ARGUMENT_ERROR -> ArgumentError,
+ * MPA_DIMENSION_MISMATCH -> DimensionMismatch, MPA_ERROR -> ErrorException; the message
+ * (same text as the reference's) is returned by mpa_last_error() on the calling thread.
+ *
+ * Buffers.  With the HIP transport, sendbuf/recvbuf/isendbuf/irecvbuf are device
+ * pointers on the coordinator's GPU; all device work the pool enqueues for the
+ * coordinator (harvest copies into recvbuf, copies of sendbuf into isendbuf) is ordered
+ * on the comm's coordinator stream (mpa_comm_set_stream), so a caller that reads recvbuf
+ * or writes sendbuf on that stream needs no further synchronisation.  With the SIM
+ * transport (host-logic tests only) they are host pointers.
+ *
+ * Threading: one coordinator thread per pool, as in the reference.  The nwait callback
+ * runs synchronously on the calling thread.  Not re-entrant per pool.
+ */
+#ifndef MPIASYNCPOOLS_H
+#define MPIASYNCPOOLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPA_ABI_VERSION 1
+
+typedef struct mpa_pool mpa_pool;
+typedef struct mpa_comm mpa_comm;
+
+enum mpa_status {
+  MPA_OK = 0,
+  MPA_ARGUMENT_ERROR = 1,     /* ArgumentError      (src/MPIAsyncPools.jl:71,73,74,197) */
+  MPA_DIMENSION_MISMATCH = 2, /* DimensionMismatch  (src/MPIAsyncPools.jl:75-77,198,199) */
+  MPA_ERROR = 3,              /* ErrorException     (src/MPIAsyncPools.jl:157) */
+  MPA_DEVICE_ERROR = 4,       /* a HIP call or a device-side check failed */
+  MPA_CALLBACK_ERROR = 5,     /* the nwait callback reported an exception */
+};
+
+enum mpa_dtype { MPA_F32 = 0, MPA_F64 = 1, MPA_BF16 = 2 };
+
+enum mpa_transport {
+  MPA_TRANSPORT_HIP = 0, /* the product: device workers on HIP streams */
+  MPA_TRANSPORT_SIM = 1, /* deterministic virtual-clock host transport, for host-logic tests */
+};
+
+enum mpa_nwait_kind { MPA_NWAIT_INT = 0, MPA_NWAIT_FN = 1, MPA_NWAIT_OTHER = 2 };
+
+enum mpa_task {
+  MPA_TASK_NONE = 0,
+  MPA_TASK_ECHO = 1,       /* reply = the received bytes (zero padded / truncated) */
+  MPA_TASK_KMAP1 = 2,      /* reply = Float64(rank)            (test/kmap1.jl:24-32) */
+  MPA_TASK_KMAP2 = 3,      /* reply = Float64[rank, t, epoch]  (test/kmap2.jl:110-132) */
+  MPA_TASK_LSQ = 4,        /* reply = A_i^T (A_i x - b_i)      (BASELINE workload) */
+  MPA_TASK_LSQ_BATCH = 5,  /* reply = A_i^T (A_i X - B_i), X cols x k (bf16 MFMA) */
+};
+
+/* nwait::Function — nwait(epoch, repochs)::Bool (src/MPIAsyncPools.jl:153).
+ * Return 1 (true), 0 (false) or a negative value if the callback raised. */
+typedef int (*mpa_nwait_fn)(void* ctx, int64_t epoch, const int64_t* repochs, int64_t n);
+
+int mpa_abi_version(void);
+const char* mpa_last_error(void);
+
+/* ---- pool: src/MPIAsyncPools.jl:24-46 -------------------------------------------- */
+/* ranks == NULL means ranks 1:n (src/MPIAsyncPools.jl:46). */
+int mpa_pool_create(int64_t n, const int64_t* ranks, int64_t epoch0, int64_t nwait, mpa_pool** out);
+void mpa_pool_destroy(mpa_pool* pool);
+int64_t mpa_pool_size(const mpa_pool* pool);
+int64_t* mpa_pool_ranks(mpa_pool* pool);
+int64_t* mpa_pool_sepochs(mpa_pool* pool);
+int64_t* mpa_pool_repochs(mpa_pool* pool);
+uint8_t* mpa_pool_active(mpa_pool* pool);
+int64_t* mpa_pool_stimestamps(mpa_pool* pool);
+double* mpa_pool_latency(mpa_pool* pool);
+int64_t* mpa_pool_nwait(mpa_pool* pool);
+int64_t* mpa_pool_epoch(mpa_pool* pool);
+
+/* ---- asyncmap! / waitall!: src/MPIAsyncPools.jl:68-188, 195-224 ------------------- */
+/* recvbuf_length is the element count of recvbuf (the reference checks
+ * `mod(length(recvbuf), n) == 0`, src/MPIAsyncPools.jl:77).  On success *repochs_out
+ * (if non-NULL) receives mpa_pool_repochs(pool): the same aliased vector the reference
+ * returns (src/MPIAsyncPools.jl:187). */
+int mpa_asyncmap(mpa_pool* pool,
+                 const void* sendbuf, size_t sendbuf_bytes,
+                 void* recvbuf, size_t recvbuf_bytes, size_t recvbuf_length,
+                 void* isendbuf, size_t isendbuf_bytes,
+                 void* irecvbuf, size_t irecvbuf_bytes,
+                 mpa_comm* comm,
+                 int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn, void* nwait_ctx,
+                 const char* nwait_typename,
+                 int64_t epoch, int64_t tag,
+                 int64_t** repochs_out);
+
+int mpa_waitall(mpa_pool* pool,
+                void* recvbuf, size_t recvbuf_bytes, size_t recvbuf_length,
+                void* irecvbuf, size_t irecvbuf_bytes,
+                int64_t** repochs_out);
+
+/* ---- comm: MPI.Comm + the worker programs ------------------------------------------ */
+/* nworkers device workers with ranks 1..nworkers (rank 0 is the coordinator).
+ * devices[w] (w = rank-1) is the HIP device of worker w; NULL = the current device. */
+int mpa_comm_create(int transport, int64_t nworkers, const int* devices, mpa_comm** out);
+void mpa_comm_destroy(mpa_comm* comm);
+int64_t mpa_comm_size(const mpa_comm* comm); /* nworkers + 1, as MPI.Comm_size */
+/* coordinator stream (hipStream_t); NULL = the device's null stream */
+int mpa_comm_set_stream(mpa_comm* comm, void* stream);
+/* worker tasks (rank in 1..nworkers) */
+int mpa_comm_set_task_kmap(mpa_comm* comm, int64_t rank, int task /* ECHO/KMAP1/KMAP2 */);
+/* A_i: rows x cols row-major with leading dimension lda (elements, lda % (16/sizeof) == 0),
+ * b_i: rows, both device pointers on the worker's device; x = cols elements and the reply
+ * g_i = cols elements, dtype MPA_F32 or MPA_F64. */
+int mpa_comm_set_task_lsq(mpa_comm* comm, int64_t rank, int dtype, int64_t rows, int64_t cols,
+                          const void* A, int64_t lda, const void* b);
+/* straggler emulation: task t (1-based) of the worker is delayed by
+ * delays_ns[(t-1) % count] before it computes; count == 0 clears the schedule */
+int mpa_comm_set_delays(mpa_comm* comm, int64_t rank, const int64_t* delays_ns, int64_t count);
+/* tasks completed (replies published) by a worker so far */
+int64_t mpa_comm_tasks_done(mpa_comm* comm, int64_t rank);
+/* control channel: wait for every outstanding task, then refuse further posts */
+int mpa_comm_shutdown(mpa_comm* comm);
+/* HIP transport: time every worker-task kernel launch with HIP events on the stream it
+ * runs on (enable = 1 / 0).  mpa_comm_timing returns, since its previous call:
+ * out[0] launches, out[1] summed kernel milliseconds, out[2] summed algorithmic bytes
+ * (A_i + b_i + x + g_i of every task in the launch). */
+int mpa_comm_set_timing(mpa_comm* comm, int enable);
+int mpa_comm_timing(mpa_comm* comm, double out[3]);
+/* SIM transport only: compute time per task and the virtual clock */
+int mpa_comm_sim_set_compute(mpa_comm* comm, int64_t compute_ns);
+int mpa_comm_sim_advance(mpa_comm* comm, int64_t dt_ns);
+int64_t mpa_comm_sim_now(const mpa_comm* comm);
+
+/* ---- coordinator-side device kernels (HIP transport; on the coordinator stream) ---- */
+/* out[c] = sum_{i=0}^{nchunks-1} weights[i] * chunk_i[c]  (fixed order, deterministic) */
+int mpa_aggregate(mpa_comm* comm, int dtype, const void* recvbuf, int64_t nchunks,
+                  int64_t chunk_elems, const double* weights, void* out);
+/* x[c] -= eta * sum_i weights[i] * chunk_i[c]   (the iterate update of the LSQ example) */
+int mpa_lsq_update(mpa_comm* comm, int dtype, void* x, const void* recvbuf, int64_t nchunks,
+                   int64_t cols, const double* weights, double eta);
+
+/* ---- synthetic data (device): Philox4x32-10 layout of DESIGN.md §Data ------------- */
+/* out[k] = unit(philox(seed, stream, e0 + k)) * scale, k < count, dtype F32/F64/BF16 */
+int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count,
+                 double scale, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPIASYNCPOOLS_H */

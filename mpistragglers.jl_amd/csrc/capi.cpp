@@ -1,0 +1,285 @@
+// extern "C" entry points declared in include/mpiasyncpools.h.  Every entry converts
+// library failures into a status code + thread-local message (mpa_last_error).
+#include <hip/hip_runtime.h>
+
+#include <new>
+
+#include "comm.hpp"
+#include "kernels.hpp"
+#include "pool.hpp"
+
+namespace mpa {
+void sim_set_compute(Comm* c, int64_t ns);
+void sim_advance(Comm* c, int64_t dt);
+int64_t sim_now(const Comm* c);
+void hip_set_stream(Comm* c, void* s);
+void* hip_get_stream(Comm* c);
+void hip_set_timing(Comm* c, bool on);
+void hip_timing(Comm* c, double out[3]);
+}  // namespace mpa
+
+struct mpa_pool {
+  mpa::Pool p;
+};
+struct mpa_comm {
+  mpa::Comm* c;
+};
+
+namespace {
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return MPA_OK;
+  } catch (const mpa::Failure& e) {
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    mpa::set_error("out of host memory");
+    return MPA_ERROR;
+  } catch (...) {
+    mpa::set_error("unexpected C++ exception");
+    return MPA_ERROR;
+  }
+}
+
+mpa::Comm& comm_of(mpa_comm* c) {
+  if (!c || !c->c) mpa::fail(MPA_ARGUMENT_ERROR, "comm is NULL");
+  return *c->c;
+}
+
+void need_hip(mpa::Comm& c) {
+  if (c.transport() != MPA_TRANSPORT_HIP) mpa::fail(MPA_ARGUMENT_ERROR, "this call needs a HIP-transport comm");
+}
+
+#define HIPCHECK_C(expr)                                                                        \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) mpa::fail(MPA_DEVICE_ERROR, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int mpa_abi_version(void) { return MPA_ABI_VERSION; }
+const char* mpa_last_error(void) { return mpa::last_error(); }
+
+int mpa_pool_create(int64_t n, const int64_t* ranks, int64_t epoch0, int64_t nwait, mpa_pool** out) {
+  return guarded([&] {
+    if (!out) mpa::fail(MPA_ARGUMENT_ERROR, "out is NULL");
+    if (n < 0) mpa::fail(MPA_ARGUMENT_ERROR, "n must be non-negative");
+    *out = new mpa_pool{mpa::Pool(n, ranks, epoch0, nwait)};
+  });
+}
+
+void mpa_pool_destroy(mpa_pool* pool) { delete pool; }
+int64_t mpa_pool_size(const mpa_pool* pool) { return pool ? pool->p.n : 0; }
+int64_t* mpa_pool_ranks(mpa_pool* pool) { return pool->p.ranks.data(); }
+int64_t* mpa_pool_sepochs(mpa_pool* pool) { return pool->p.sepochs.data(); }
+int64_t* mpa_pool_repochs(mpa_pool* pool) { return pool->p.repochs.data(); }
+uint8_t* mpa_pool_active(mpa_pool* pool) { return pool->p.active.data(); }
+int64_t* mpa_pool_stimestamps(mpa_pool* pool) { return pool->p.stimestamps.data(); }
+double* mpa_pool_latency(mpa_pool* pool) { return pool->p.latency.data(); }
+int64_t* mpa_pool_nwait(mpa_pool* pool) { return &pool->p.nwait; }
+int64_t* mpa_pool_epoch(mpa_pool* pool) { return &pool->p.epoch; }
+
+int mpa_asyncmap(mpa_pool* pool, const void* sendbuf, size_t sendbuf_bytes, void* recvbuf, size_t recvbuf_bytes,
+                 size_t recvbuf_length, void* isendbuf, size_t isendbuf_bytes, void* irecvbuf,
+                 size_t irecvbuf_bytes, mpa_comm* comm, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
+                 void* nwait_ctx, const char* nwait_typename, int64_t epoch, int64_t tag, int64_t** repochs_out) {
+  return guarded([&] {
+    if (!pool) mpa::fail(MPA_ARGUMENT_ERROR, "pool is NULL");
+    if (nwait_kind == MPA_NWAIT_FN && !nwait_fn) mpa::fail(MPA_ARGUMENT_ERROR, "nwait function is NULL");
+    mpa::AsyncmapArgs a{sendbuf, sendbuf_bytes, recvbuf, recvbuf_bytes, recvbuf_length, isendbuf, isendbuf_bytes,
+                        irecvbuf, irecvbuf_bytes, comm ? comm->c : nullptr, nwait_kind, nwait, nwait_fn,
+                        nwait_ctx, nwait_typename, epoch, tag};
+    mpa::asyncmap(pool->p, a);
+    if (repochs_out) *repochs_out = pool->p.repochs.data();
+  });
+}
+
+int mpa_waitall(mpa_pool* pool, void* recvbuf, size_t recvbuf_bytes, size_t recvbuf_length, void* irecvbuf,
+                size_t irecvbuf_bytes, int64_t** repochs_out) {
+  return guarded([&] {
+    if (!pool) mpa::fail(MPA_ARGUMENT_ERROR, "pool is NULL");
+    mpa::waitall(pool->p, recvbuf, recvbuf_bytes, recvbuf_length, irecvbuf, irecvbuf_bytes);
+    if (repochs_out) *repochs_out = pool->p.repochs.data();
+  });
+}
+
+int mpa_comm_create(int transport, int64_t nworkers, const int* devices, mpa_comm** out) {
+  return guarded([&] {
+    if (!out) mpa::fail(MPA_ARGUMENT_ERROR, "out is NULL");
+    if (nworkers < 0) mpa::fail(MPA_ARGUMENT_ERROR, "nworkers must be non-negative");
+    mpa::Comm* c = nullptr;
+    if (transport == MPA_TRANSPORT_HIP) c = mpa::make_hip_comm(nworkers, devices);
+    else if (transport == MPA_TRANSPORT_SIM) c = mpa::make_sim_comm(nworkers);
+    else mpa::fail(MPA_ARGUMENT_ERROR, "unknown transport %d", transport);
+    *out = new mpa_comm{c};
+  });
+}
+
+void mpa_comm_destroy(mpa_comm* comm) {
+  if (!comm) return;
+  delete comm->c;
+  delete comm;
+}
+
+int64_t mpa_comm_size(const mpa_comm* comm) { return comm && comm->c ? comm->c->nworkers() + 1 : 0; }
+
+int mpa_comm_set_stream(mpa_comm* comm, void* stream) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    mpa::hip_set_stream(&c, stream);
+  });
+}
+
+int mpa_comm_set_task_kmap(mpa_comm* comm, int64_t rank, int task) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    if (task != MPA_TASK_ECHO && task != MPA_TASK_KMAP1 && task != MPA_TASK_KMAP2)
+      mpa::fail(MPA_ARGUMENT_ERROR, "task must be MPA_TASK_ECHO, MPA_TASK_KMAP1 or MPA_TASK_KMAP2");
+    mpa::TaskSpec& t = c.task(rank);
+    const mpa::TaskSpec saved = t;
+    t.kind = task;
+    try {
+      c.on_task_changed(rank);
+    } catch (...) {
+      t = saved;
+      throw;
+    }
+  });
+}
+
+int mpa_comm_set_task_lsq(mpa_comm* comm, int64_t rank, int dtype, int64_t rows, int64_t cols, const void* A,
+                          int64_t lda, const void* b) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    if (dtype != MPA_F32 && dtype != MPA_F64) mpa::fail(MPA_ARGUMENT_ERROR, "least squares: dtype must be F32 or F64");
+    if (rows < 0 || cols <= 0) mpa::fail(MPA_ARGUMENT_ERROR, "least squares: bad shape");
+    if (rows > 0 && (!A || !b)) mpa::fail(MPA_ARGUMENT_ERROR, "least squares: A and b must be device pointers");
+    mpa::TaskSpec& t = c.task(rank);
+    const mpa::TaskSpec saved = t;
+    t.kind = MPA_TASK_LSQ;
+    t.dtype = dtype;
+    t.rows = rows;
+    t.cols = cols;
+    t.lda = lda;
+    t.A = A;
+    t.b = b;
+    try {
+      c.on_task_changed(rank);
+    } catch (...) {
+      t = saved;
+      throw;
+    }
+  });
+}
+
+int mpa_comm_set_delays(mpa_comm* comm, int64_t rank, const int64_t* delays_ns, int64_t count) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    if (count < 0 || (count > 0 && !delays_ns)) mpa::fail(MPA_ARGUMENT_ERROR, "bad delay schedule");
+    for (int64_t k = 0; k < count; ++k)
+      if (delays_ns[k] < 0) mpa::fail(MPA_ARGUMENT_ERROR, "delays must be non-negative");
+    c.task(rank).delays_ns.assign(delays_ns, delays_ns + count);
+  });
+}
+
+int64_t mpa_comm_tasks_done(mpa_comm* comm, int64_t rank) {
+  int64_t r = -1;
+  const int rc = guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    c.task(rank);
+    r = c.tasks_done(rank);
+  });
+  return rc == MPA_OK ? r : -1;
+}
+
+int mpa_comm_shutdown(mpa_comm* comm) {
+  return guarded([&] { comm_of(comm).shutdown(); });
+}
+
+int mpa_comm_set_timing(mpa_comm* comm, int enable) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    mpa::hip_set_timing(&c, enable != 0);
+  });
+}
+
+int mpa_comm_timing(mpa_comm* comm, double out[3]) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    if (!out) mpa::fail(MPA_ARGUMENT_ERROR, "out is NULL");
+    mpa::hip_timing(&c, out);
+  });
+}
+
+int mpa_comm_sim_set_compute(mpa_comm* comm, int64_t compute_ns) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    if (c.transport() != MPA_TRANSPORT_SIM) mpa::fail(MPA_ARGUMENT_ERROR, "not a SIM comm");
+    mpa::sim_set_compute(&c, compute_ns);
+  });
+}
+
+int mpa_comm_sim_advance(mpa_comm* comm, int64_t dt_ns) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    if (c.transport() != MPA_TRANSPORT_SIM) mpa::fail(MPA_ARGUMENT_ERROR, "not a SIM comm");
+    mpa::sim_advance(&c, dt_ns);
+  });
+}
+
+int64_t mpa_comm_sim_now(const mpa_comm* comm) {
+  if (!comm || !comm->c || comm->c->transport() != MPA_TRANSPORT_SIM) return -1;
+  return mpa::sim_now(comm->c);
+}
+
+static int aggregate_impl(mpa_comm* comm, int dtype, const void* recvbuf, int64_t n, int64_t elems,
+                          const double* weights, void* out, int update, double eta) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    if (dtype != MPA_F32 && dtype != MPA_F64) mpa::fail(MPA_ARGUMENT_ERROR, "aggregate: dtype must be F32 or F64");
+    if (n < 0 || n > mpa::kMaxAggregate) mpa::fail(MPA_ARGUMENT_ERROR, "aggregate: 0 <= nchunks <= %d", mpa::kMaxAggregate);
+    if (elems < 0 || (n > 0 && !weights) || !out || (n > 0 && !recvbuf))
+      mpa::fail(MPA_ARGUMENT_ERROR, "aggregate: bad arguments");
+    mpa::AggregateArgs a{};
+    a.chunks = recvbuf;
+    a.out = out;
+    a.n = n;
+    a.elems = elems;
+    a.stride = elems;
+    a.eta = eta;
+    a.update = update;
+    for (int64_t i = 0; i < n; ++i) a.w[i] = weights[i];
+    HIPCHECK_C(mpa::launch_aggregate(dtype, a, static_cast<hipStream_t>(mpa::hip_get_stream(&c))));
+  });
+}
+
+int mpa_aggregate(mpa_comm* comm, int dtype, const void* recvbuf, int64_t nchunks, int64_t chunk_elems,
+                  const double* weights, void* out) {
+  return aggregate_impl(comm, dtype, recvbuf, nchunks, chunk_elems, weights, out, 0, 0.0);
+}
+
+int mpa_lsq_update(mpa_comm* comm, int dtype, void* x, const void* recvbuf, int64_t nchunks, int64_t cols,
+                   const double* weights, double eta) {
+  return aggregate_impl(comm, dtype, recvbuf, nchunks, cols, weights, x, 1, eta);
+}
+
+int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count, double scale,
+                 void* hip_stream) {
+  return guarded([&] {
+    if (dtype != MPA_F32 && dtype != MPA_F64 && dtype != MPA_BF16) mpa::fail(MPA_ARGUMENT_ERROR, "generate: bad dtype");
+    if (count < 0 || (count > 0 && !out)) mpa::fail(MPA_ARGUMENT_ERROR, "generate: bad arguments");
+    HIPCHECK_C(mpa::launch_generate(out, dtype, seed, stream, e0, count, scale, static_cast<hipStream_t>(hip_stream)));
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// Transport-facing interface of a communicator (the `comm::MPI.Comm` argument of
+// asyncmap!, src/MPIAsyncPools.jl:68) and the worker tasks registered on it.
+//
+// The pool state machine (pool.cpp) drives a Comm through the MPI point-to-point verbs
+// the reference uses: Isend+Irecv! (:137-138, :182-183) -> post(), Test! (:99) -> test(),
+// Waitany! (:161) -> waitany(), Waitall! (:212) -> waitall(), and the byte copy
+// `recvbufs[i] .= irecvbufs[i]` (:108, :167, :216) -> harvest().  A transport may defer
+// harvest copies and posts until flush(); the pool calls flush() wherever the reference's
+// program order makes a deferred copy observable (before a worker's irecv chunk can be
+// overwritten) and end_call() before returning to the caller.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "common.hpp"
+
+namespace mpa {
+
+struct CallBufs {
+  const uint8_t* sendbuf = nullptr;
+  size_t sl = 0;  // bytes per send slot (sizeof(sendbuf), :80)
+  uint8_t* recvbuf = nullptr;
+  uint8_t* isendbuf = nullptr;
+  uint8_t* irecvbuf = nullptr;
+  size_t rl = 0;  // bytes per recv chunk (:81)
+  int64_t n = 0;  // pool size
+};
+
+struct TaskSpec {
+  int kind = MPA_TASK_NONE;
+  int dtype = MPA_F32;
+  int64_t rows = 0, cols = 0, lda = 0;
+  const void* A = nullptr;
+  const void* b = nullptr;
+  std::vector<int64_t> delays_ns;
+};
+
+class Comm {
+ public:
+  explicit Comm(int64_t nworkers) : nworkers_(nworkers), tasks_(size_t(nworkers)) {}
+  virtual ~Comm() = default;
+  virtual int transport() const = 0;
+  int64_t nworkers() const { return nworkers_; }
+
+  // ---- per-call protocol (pool.cpp) ----
+  virtual void begin_call(const CallBufs& b) = 0;
+  virtual void post(int64_t i, int64_t rank, int64_t tag) = 0;
+  virtual void harvest(int64_t i, int64_t rank) = 0;
+  virtual bool test(int64_t i, int64_t rank) = 0;
+  virtual int64_t waitany(int64_t n, const int64_t* ranks, const uint8_t* live) = 0;
+  virtual void waitall(int64_t n, const int64_t* ranks, const uint8_t* live) = 0;
+  virtual void flush() = 0;
+  virtual void end_call() = 0;
+  virtual uint64_t now_ns() = 0;
+
+  // ---- worker registration ----
+  TaskSpec& task(int64_t rank) {
+    if (rank < 1 || rank > nworkers_) fail(MPA_ARGUMENT_ERROR, "rank %lld is not a worker rank of this comm (1:%lld)",
+                                           (long long)rank, (long long)nworkers_);
+    return tasks_[size_t(rank - 1)];
+  }
+  virtual void on_task_changed(int64_t rank) { (void)rank; }
+  virtual int64_t tasks_done(int64_t rank) = 0;
+  virtual void shutdown() = 0;
+  bool is_shutdown() const { return shutdown_; }
+
+ protected:
+  int64_t nworkers_;
+  std::vector<TaskSpec> tasks_;
+  bool shutdown_ = false;
+};
+
+Comm* make_sim_comm(int64_t nworkers);
+Comm* make_hip_comm(int64_t nworkers, const int* devices);
+
+}  // namespace mpa

@@ -1,0 +1,94 @@
+// Host-callable launchers of the gfx950 kernels (kernels.hip).  All launches are
+// asynchronous on the given stream; shapes are validated by the caller (transport_hip.cpp)
+// before a launch, so a kernel never indexes outside the buffers it is given.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mpa {
+
+constexpr int kMaxExchangeItems = 64;
+
+struct ExchangeArgs {
+  const uint8_t* sendbuf;
+  uint8_t* isendbuf;
+  uint64_t sl;
+  uint8_t* recvbuf;
+  const uint8_t* irecvbuf;
+  uint64_t rl;
+  int npost, nharv;
+  int bpp, bph;      // blocks per post item / per harvest item
+  uint64_t ppart, hpart;  // bytes per block (multiple of 16)
+  int16_t post[kMaxExchangeItems];
+  int16_t harv[kMaxExchangeItems];
+};
+hipError_t launch_exchange(const ExchangeArgs& a, hipStream_t s);
+
+// completion protocol shared by every worker task kernel
+struct Publish {
+  unsigned long long* flag;  // host-pinned: seq of the last completed task of the worker
+  unsigned int* err;         // host-pinned: first device-side error code (0 = none)
+  unsigned long long seq;
+  unsigned long long spin_ticks;  // bound on any in-kernel wait (s_memrealtime ticks)
+};
+
+// One worker task of a least-squares launch.
+struct LsqTask {
+  const void* A;
+  const void* b;
+  const void* x;
+  void* out;
+  void* slab;       // [grid][cols_pad] partial sums (T)
+  uint32_t* ctr;    // [2] monotonic arrival counters (device memory)
+  unsigned long long* flag;  // host-pinned completion word of the worker
+  unsigned long long seq;
+  int64_t rows, lda;
+  int cols, grid;
+};
+
+// Several workers dispatched by the same flush run as ONE launch: workgroups
+// [block0[t], block0[t+1]) belong to task t.  All tasks share (dtype, cols_pad).
+constexpr int kMaxLsqTasks = 16;
+struct LsqBatch {
+  int ntasks;
+  unsigned* err;
+  unsigned long long spin_ticks;
+  int block0[kMaxLsqTasks + 1];
+  LsqTask t[kMaxLsqTasks];
+};
+// Returns hipErrorInvalidValue if no kernel variant covers (dtype, cols).
+hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s);
+// Shape helpers for the launcher's variant table.
+int lsq_cols_pad(int dtype, int cols);  // 0 if unsupported
+int lsq_reducers(int dtype, int cols);
+int lsq_rows_per_wave_iter(int dtype, int cols);
+
+struct KmapArgs {
+  int kind;
+  double rank;
+  const uint8_t* x;
+  uint64_t sl;
+  uint8_t* out;
+  uint64_t rl;
+  Publish pub;
+};
+hipError_t launch_kmap(const KmapArgs& a, hipStream_t s);
+
+hipError_t launch_delay(unsigned long long ticks, hipStream_t s);
+
+constexpr int kMaxAggregate = 256;
+struct AggregateArgs {
+  const void* chunks;
+  void* out;     // aggregate: out = sum w_i c_i ; update: out (= x) -= eta * sum w_i c_i
+  int64_t n, elems, stride;
+  double eta;
+  int update;
+  double w[kMaxAggregate];
+};
+hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s);
+
+hipError_t launch_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count,
+                           double scale, hipStream_t s);
+
+}  // namespace mpa

@@ -1,0 +1,159 @@
+"""Communicators: the `comm::MPI.Comm` argument of asyncmap! plus the worker programs.
+
+In the reference, rank 0 of MPI.COMM_WORLD is the coordinator and ranks 1..n run a
+worker program (examples/iterative_example.jl:55-82, test/kmap1.jl:23-33,
+test/kmap2.jl:110-132).  Here a communicator owns n device workers with ranks 1..n; each
+worker runs a registered task kernel on its own HIP stream:
+
+    comm = DeviceComm(n)                      # HIP transport, current GPU
+    comm.set_task(rank, "kmap2")              # the reference's test worker programs
+    comm.set_task_lsq(rank, A_i, b_i)         # g_i = A_i^T (A_i x - b_i)
+    comm.set_delays(rank, delays_ns)          # straggler emulation
+
+`SimComm` is a deterministic virtual-clock host transport used only to test the pool
+state machine without a GPU; it is never chosen implicitly.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _capi
+from ._capi import lib
+from .pool import ArgumentError, buffer_info, check
+
+_TASKS = {"echo": _capi.MPA_TASK_ECHO, "kmap1": _capi.MPA_TASK_KMAP1, "kmap2": _capi.MPA_TASK_KMAP2}
+_DTYPES = {"float32": _capi.MPA_F32, "float64": _capi.MPA_F64, "torch.float32": _capi.MPA_F32,
+           "torch.float64": _capi.MPA_F64, "bfloat16": _capi.MPA_BF16, "torch.bfloat16": _capi.MPA_BF16}
+
+
+def dtype_code(a):
+    return _DTYPES[str(a.dtype)]
+
+
+class _Comm:
+    transport = None
+
+    def __init__(self, nworkers, devices=None):
+        h = C.c_void_p()
+        dev = None
+        if devices is not None:
+            dev = (C.c_int * nworkers)(*devices)
+        check(lib().mpa_comm_create(self.transport, int(nworkers), dev, C.byref(h)))
+        self._h = h
+        self.nworkers = int(nworkers)
+        self._keep = {}
+
+    def size(self):
+        """MPI.Comm_size: workers + the coordinator."""
+        return int(lib().mpa_comm_size(self._h))
+
+    def set_task(self, rank, task):
+        check(lib().mpa_comm_set_task_kmap(self._h, int(rank), _TASKS[task]))
+
+    def set_delays(self, rank, delays_ns):
+        d = np.ascontiguousarray(delays_ns, dtype=np.int64)
+        check(lib().mpa_comm_set_delays(self._h, int(rank), d.ctypes.data if d.size else None, d.size))
+
+    def tasks_done(self, rank):
+        return int(lib().mpa_comm_tasks_done(self._h, int(rank)))
+
+    def shutdown(self):
+        """Control channel (examples/iterative_example.jl:49-52): drain, then stop."""
+        check(lib().mpa_comm_shutdown(self._h))
+
+    def _before_call(self, sendbuf):
+        pass
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib().mpa_comm_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceComm(_Comm):
+    """HIP transport: workers are task kernels on per-worker streams of the current GPU.
+
+    Buffers passed to asyncmap_/waitall_ with this comm are torch CUDA tensors on the
+    coordinator's GPU; the pool's copies are ordered on torch's current stream."""
+
+    transport = _capi.MPA_TRANSPORT_HIP
+
+    def __init__(self, nworkers, devices=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("DeviceComm needs a GPU (HIP); no device is visible")
+        torch.cuda.init()
+        super().__init__(nworkers, devices)
+
+    def _before_call(self, sendbuf):
+        import torch
+        check(lib().mpa_comm_set_stream(self._h, C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+
+    def set_task_lsq(self, rank, A, b, cols=None, lda=None):
+        """g = A^T (A x - b) with A (rows x cols, row-major, leading dim lda) and b on the GPU."""
+        if A.dim() != 2 or b.dim() != 1 or A.shape[0] != b.shape[0]:
+            raise ArgumentError("A must be rows x lda and b must have rows elements")
+        if A.dtype != b.dtype:
+            raise ArgumentError("A and b must have the same dtype")
+        rows, ld = A.shape
+        cols = ld if cols is None else int(cols)
+        lda = ld if lda is None else int(lda)
+        check(lib().mpa_comm_set_task_lsq(self._h, int(rank), dtype_code(A), int(rows), cols,
+                                          C.c_void_p(A.data_ptr()), lda, C.c_void_p(b.data_ptr())))
+        self._keep[int(rank)] = (A, b)
+
+    def set_timing(self, enable):
+        """Time every least-squares launch with HIP events on its own stream."""
+        check(lib().mpa_comm_set_timing(self._h, 1 if enable else 0))
+
+    def timing(self):
+        """(launches, kernel_ms, algorithmic_bytes) since the previous call."""
+        out = (C.c_double * 3)()
+        check(lib().mpa_comm_timing(self._h, out))
+        return int(out[0]), float(out[1]), float(out[2])
+
+    def aggregate(self, recvbuf, nchunks, weights, out):
+        """out = sum_i weights[i] * chunk_i of recvbuf (device kernel, fixed order)."""
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        chunk = recvbuf.numel() // nchunks
+        self._before_call(out)
+        check(lib().mpa_aggregate(self._h, dtype_code(recvbuf), C.c_void_p(recvbuf.data_ptr()), int(nchunks),
+                                  int(chunk), w.ctypes.data, C.c_void_p(out.data_ptr())))
+
+    def lsq_update(self, x, recvbuf, nchunks, weights, eta):
+        """x -= eta * sum_i weights[i] * g_i (device kernel, fixed order)."""
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        self._before_call(x)
+        check(lib().mpa_lsq_update(self._h, dtype_code(x), C.c_void_p(x.data_ptr()),
+                                   C.c_void_p(recvbuf.data_ptr()), int(nchunks), int(x.numel()),
+                                   w.ctypes.data, float(eta)))
+
+
+class SimComm(_Comm):
+    """Virtual-clock host transport (tests of the state machine only); numpy buffers."""
+
+    transport = _capi.MPA_TRANSPORT_SIM
+
+    def set_compute(self, ns):
+        check(lib().mpa_comm_sim_set_compute(self._h, int(ns)))
+
+    def advance(self, dt_ns):
+        check(lib().mpa_comm_sim_advance(self._h, int(dt_ns)))
+
+    @property
+    def now(self):
+        return int(lib().mpa_comm_sim_now(self._h))
+
+
+def generate(out, seed, stream, e0, scale=1.0):
+    """Fill a CUDA tensor with the Philox4x32-10 synthetic layout."""
+    import torch
+    check(lib().mpa_generate(C.c_void_p(out.data_ptr()), dtype_code(out), int(seed), int(stream), int(e0),
+                             int(out.numel()), float(scale), C.c_void_p(torch.cuda.current_stream().cuda_stream)))

@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+# One HSA queue per stream: HIP serialises every kernel of streams that share a hardware
+# queue, so a straggler's delay kernel would otherwise hold back unrelated workers.  Must be
+# set before the HIP runtime initialises (DESIGN.md §Streams and queues).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "mpistragglers.jl_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def built():
+    """Build the oracle (gcc) and the HIP library (hipcc) once per session if missing."""
+    import subprocess
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_build", "liboracle.so")):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"])
+    if not os.path.exists(os.path.join(ROOT, "mpistragglers.jl_amd", "_build", "libmpiasyncpools.so")):
+        subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "mpistragglers.jl_amd")])
+    return True

@@ -1,0 +1,302 @@
+"""GPU parity tests: the HIP path (libmpiasyncpools.so through its C ABI) against the oracle.
+
+  * the reference's own tests (test/kmap1.jl, test/kmap2.jl) on device workers;
+  * golden traces (tests/golden/traces.json, `gpu_sep_*`): repochs / active / recvbuf
+    bit-exact under the same straggler schedule, injected by the delay kernel;
+  * the least-squares shard kernel against the fp64 numpy oracle (rel 1e-5 fp32,
+    1e-12 fp64, BASELINE.json north_star), small shapes incl. ragged rows and masked
+    columns, and the full BASELINE c2 shape against a torch fp64 reference;
+  * the device data generator bit-exact against oracle/lsq.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def M(built):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    import mpiasyncpools
+    return mpiasyncpools
+
+
+@pytest.fixture(scope="module")
+def torch_mod(M):
+    import torch
+    return torch
+
+
+def _dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def test_kmap1(M, torch_mod):
+    torch = torch_mod
+    nworkers = 2
+    comm = M.DeviceComm(nworkers)
+    for r in range(1, nworkers + 1):
+        comm.set_task(r, "kmap1")
+    pool = M.MPIAsyncPool(nworkers)
+    sendbuf = torch.full((1,), 3.14, dtype=torch.float64, device="cuda")
+    isendbuf = torch.zeros(nworkers, dtype=torch.float64, device="cuda")
+    recvbuf = torch.empty(nworkers, dtype=torch.float64, device="cuda")
+    irecvbuf = recvbuf.clone()
+    M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=nworkers, tag=0)
+    assert recvbuf.cpu().tolist() == [1.0, 2.0]                    # kmap1.jl:22
+    assert isendbuf.cpu().tolist() == [3.14, 3.14]                 # kmap1.jl:30
+
+
+@pytest.mark.parametrize("nranks", [3, 10])
+def test_kmap2(M, torch_mod, nranks):
+    """test/kmap2.jl end to end on device workers; delays = the reference's distribution / 10."""
+    import time
+    torch = torch_mod
+    nworkers = nranks - 1
+    rng = np.random.default_rng(nranks)
+    comm = M.DeviceComm(nworkers)
+    for r in range(1, nworkers + 1):
+        comm.set_task(r, "kmap2")
+        comm.set_delays(r, (np.maximum(rng.random(256) / 10, 0.005) * 1e8).astype(np.int64))
+    pool = M.MPIAsyncPool(nworkers)
+    assert list(pool.ranks) == list(range(1, nworkers + 1))
+    sendbuf = torch.empty(1, dtype=torch.float64, device="cuda")
+    isendbuf = torch.zeros(nworkers, dtype=torch.float64, device="cuda")
+    recvbuf = torch.empty(3 * nworkers, dtype=torch.float64, device="cuda")
+    irecvbuf = recvbuf.clone()
+    nwait = 2
+    for epoch in range(1, 101):
+        sendbuf.fill_(epoch)
+        repochs = M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=nwait, tag=0)
+        rb = recvbuf.cpu().numpy().reshape(nworkers, 3)
+        fresh = 0
+        for i in range(nworkers):
+            if repochs[i] == 0:
+                continue
+            if repochs[i] == epoch:
+                fresh += 1
+            assert rb[i, 2] == repochs[i]
+            assert rb[i, 0] == i + 1
+        assert fresh >= nwait
+    for _ in range(100):
+        M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=1, tag=0)
+        M.waitall_(pool, recvbuf, irecvbuf)
+        assert not pool.active.any()
+    f = lambda epoch, repochs: bool(repochs[0] == epoch)
+    for _ in range(101, 201):
+        t0 = time.perf_counter()
+        repochs = M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=f, tag=0)
+        delay = time.perf_counter() - t0
+        assert repochs[0] == pool.epoch
+        assert abs(delay - pool.latency[0]) <= 1e-3
+    # t counts the tasks each worker served (kmap2.jl:116-118)
+    M.waitall_(pool, recvbuf, irecvbuf)
+    rb = recvbuf.cpu().numpy().reshape(nworkers, 3)
+    for i in range(nworkers):
+        assert rb[i, 1] == comm.tasks_done(i + 1)
+    comm.shutdown()
+
+
+GOLD = [s for s in json.load(open(os.path.join(GOLDEN, "traces.json")))["scenarios"] if s["name"].startswith("gpu_sep")]
+
+
+@pytest.mark.parametrize("name", [s["name"] for s in GOLD])
+def test_golden_traces_on_device(M, torch_mod, name):
+    """repochs / active / recvbuf bit-exact against the oracle's trace under the same
+    straggler schedule (completion times >= 4 ms apart, so the order is physical)."""
+    import importlib.util
+    torch = torch_mod
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    sc = next(s for s in GOLD if s["name"] == name)
+    n = sc["n"]
+    dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(n, -1)
+    comm = M.DeviceComm(n)
+    for r in range(1, n + 1):
+        comm.set_task(r, "kmap2")
+        comm.set_delays(r, dur[r - 1])
+    pool = M.MPIAsyncPool(n)
+    send = torch.zeros(1, dtype=torch.float64, device="cuda")
+    isend = torch.zeros(n, dtype=torch.float64, device="cuda")
+    recv = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    irecv = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    for k, (op, ref) in enumerate(zip(sc["ops"], sc["results"])):
+        if op["op"] == "waitall":
+            M.waitall_(pool, recv, irecv)
+        else:
+            send.fill_(op["send"])
+            nw = op["nwait"]
+            M.asyncmap_(pool, send, recv, isend, irecv, comm, nwait=mg.predicate(nw) if isinstance(nw, str) else nw)
+        assert pool.repochs.tolist() == ref["repochs"], (name, k)
+        assert pool.active.astype(int).tolist() == ref["active"], (name, k)
+        assert recv.cpu().tolist() == ref["recv"], (name, k)
+        lat = np.asarray(ref["latency_ns"]) / 1e9
+        assert np.all(np.abs(pool.latency - lat) < 3e-3), (name, k, pool.latency, lat)
+
+
+def _lsq_case(M, torch, dtype, rows, cols, lda=None, seed=3, nworkers=1, grid=None):
+    import lsq
+    lda = cols if lda is None else lda
+    tname = "f32" if dtype == "f32" else "f64"
+    tdt = torch.float32 if dtype == "f32" else torch.float64
+    A = np.zeros((rows, lda), dtype=np.float32 if dtype == "f32" else np.float64)
+    A[:, :cols] = lsq.gen_matrix(seed, 0, rows, cols, tname)
+    b = lsq.gen_vector(seed, 0, rows, tname)
+    x = lsq.gen_vector(seed, 0, cols, tname, stream=lsq.STREAM_X, scale=0.5)
+    comm = M.DeviceComm(nworkers)
+    Ad, bd = _dev(torch, A), _dev(torch, b)
+    for r in range(1, nworkers + 1):
+        comm.set_task_lsq(r, Ad, bd, cols=cols, lda=lda)
+    pool = M.MPIAsyncPool(nworkers)
+    send = _dev(torch, x)
+    isend = torch.zeros(nworkers * cols, dtype=tdt, device="cuda")
+    recv = torch.zeros(nworkers * cols, dtype=tdt, device="cuda")
+    irecv = torch.zeros_like(recv)
+    M.asyncmap_(pool, send, recv, isend, irecv, comm, nwait=nworkers)
+    g_ref = lsq.shard_gradient(A[:, :cols], b, x)
+    out = recv.cpu().numpy().reshape(nworkers, cols)
+    return out, g_ref, (comm, pool, send, recv, isend, irecv)
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 256), (37, 256), (1000, 512), (4099, 1024), (2048, 2048),
+                                       (777, 1000), (513, 100), (5000, 1536)])
+def test_lsq_f32(M, torch_mod, rows, cols):
+    out, g_ref, _ = _lsq_case(M, torch_mod, "f32", rows, cols, lda=((cols + 3) // 4) * 4)
+    err = np.linalg.norm(out[0] - g_ref) / np.linalg.norm(g_ref)
+    assert err <= 1e-5, err
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 128), (300, 256), (1025, 1024), (999, 2048), (64, 130)])
+def test_lsq_f64(M, torch_mod, rows, cols):
+    out, g_ref, _ = _lsq_case(M, torch_mod, "f64", rows, cols, lda=((cols + 1) // 2) * 2)
+    err = np.linalg.norm(out[0] - g_ref) / np.linalg.norm(g_ref)
+    assert err <= 1e-12, err
+
+
+def test_lsq_padded_lda_and_determinism(M, torch_mod):
+    torch = torch_mod
+    out, g_ref, st = _lsq_case(M, torch, "f32", 3000, 1000, lda=1024, nworkers=3)
+    comm, pool, send, recv, isend, irecv = st
+    assert np.linalg.norm(out[0] - g_ref) / np.linalg.norm(g_ref) <= 1e-5
+    # every worker computed the same shard: identical bits (fixed-order reduction)
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+    assert np.array_equal(out[0].view(np.uint32), out[2].view(np.uint32))
+    first = recv.clone()
+    for _ in range(3):
+        M.asyncmap_(pool, send, recv, isend, irecv, comm, nwait=3)
+        assert torch.equal(first.view(torch.int32), recv.view(torch.int32))
+
+
+def test_lsq_gradient_descent_chunks_match_their_epochs(M, torch_mod):
+    """Asyncmap with least-squares workers and stragglers: each chunk i equals the
+    gradient of the iterate sent at epoch repochs[i] (kmap2.jl:84, numerically)."""
+    import lsq
+    torch = torch_mod
+    n, rows, cols, seed = 4, 2048, 512, 11
+    comm = M.DeviceComm(n)
+    A = lsq.gen_matrix(seed, 0, n * rows, cols, "f32")
+    b = lsq.gen_vector(seed, 0, n * rows, "f32")
+    keep = []
+    rng = np.random.default_rng(5)
+    for r in range(1, n + 1):
+        Ad, bd = _dev(torch, A[(r - 1) * rows:r * rows]), _dev(torch, b[(r - 1) * rows:r * rows])
+        keep.append((Ad, bd))
+        comm.set_task_lsq(r, Ad, bd)
+        comm.set_delays(r, rng.integers(0, 6, size=16) * 1_000_000)
+    pool = M.MPIAsyncPool(n)
+    x = torch.zeros(cols, dtype=torch.float32, device="cuda")
+    isend = torch.zeros(n * cols, dtype=torch.float32, device="cuda")
+    recv = torch.zeros(n * cols, dtype=torch.float32, device="cuda")
+    irecv = torch.zeros_like(recv)
+    sent = {}
+    for epoch in range(1, 16):
+        sent[epoch] = x.cpu().numpy().copy()
+        rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=2)
+        chunks = recv.cpu().numpy().reshape(n, cols)
+        for i in range(n):
+            if rep[i] == 0:
+                continue
+            xs = sent[int(rep[i])]
+            g = lsq.shard_gradient(A[i * rows:(i + 1) * rows], b[i * rows:(i + 1) * rows], xs)
+            assert lsq.rel_err(chunks[i], g) <= 1e-5, (epoch, i)
+        w = (rep == epoch).astype(np.float64) * (n / max(1, int((rep == epoch).sum())))
+        comm.lsq_update(x, recv, n, w, 0.05)
+    M.waitall_(pool, recv, irecv)
+
+
+def test_aggregate_and_update(M, torch_mod):
+    torch = torch_mod
+    rng = np.random.default_rng(0)
+    comm = M.DeviceComm(1)
+    for dt, tdt, tol in ((np.float32, torch.float32, 1e-6), (np.float64, torch.float64, 1e-15)):
+        n, c = 7, 1000
+        chunks = rng.standard_normal((n, c)).astype(dt)
+        w = rng.standard_normal(n)
+        w[2] = 0.0
+        out = torch.zeros(c, dtype=tdt, device="cuda")
+        comm.aggregate(_dev(torch, chunks.ravel()), n, w, out)
+        ref = (w[:, None] * chunks.astype(np.float64)).sum(0)
+        assert np.max(np.abs(out.cpu().numpy() - ref)) <= tol * np.max(np.abs(ref)) * 10
+        x0 = rng.standard_normal(c).astype(dt)
+        x = _dev(torch, x0)
+        comm.lsq_update(x, _dev(torch, chunks.ravel()), n, w, 0.1)
+        assert np.max(np.abs(x.cpu().numpy() - (x0 - 0.1 * ref))) <= tol * 10 * (1 + np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64", "bf16"])
+def test_generate_bit_exact(M, torch_mod, dtype):
+    import lsq
+    torch = torch_mod
+    tdt = {"f32": torch.float32, "f64": torch.float64, "bf16": torch.bfloat16}[dtype]
+    for e0, cnt, scale in ((0, 4096, 1 / 32), (5, 1001, 0.7), (2**35 + 3, 333, 1.0)):
+        out = torch.empty(cnt, dtype=tdt, device="cuda")
+        M.generate(out, 42, 0, e0, scale)
+        ref = lsq.gen_vector(42, e0, cnt, dtype, stream=0,
+                             scale=np.float64(scale) if dtype == "f64" else np.float32(scale))
+        got = out.cpu()
+        if dtype == "bf16":
+            assert np.array_equal(got.view(torch.int16).numpy().view(np.uint16), ref)
+        elif dtype == "f32":
+            assert np.array_equal(got.numpy().view(np.uint32), ref.view(np.uint32))
+        else:
+            assert np.array_equal(got.numpy().view(np.uint64), ref.view(np.uint64))
+
+
+def test_full_size_c2_against_torch_fp64(M, torch_mod):
+    """BASELINE c2 shape (A 2^20 x 1024 fp32, 8 workers): every worker's g_i against a
+    torch fp64 computation of A_i^T(A_i x - b_i) on the same device data (rel 1e-5)."""
+    torch = torch_mod
+    n, rows, cols, seed = 8, 1 << 20, 1024, 1234
+    per = rows // n
+    comm = M.DeviceComm(n)
+    A = torch.empty(rows, cols, dtype=torch.float32, device="cuda")
+    b = torch.empty(rows, dtype=torch.float32, device="cuda")
+    M.generate(A, seed, 0, 0, float(np.float32(1 / np.sqrt(cols))))
+    M.generate(b, seed, 1, 0, 1.0)
+    for r in range(1, n + 1):
+        comm.set_task_lsq(r, A[(r - 1) * per:r * per], b[(r - 1) * per:r * per])
+    x = torch.empty(cols, dtype=torch.float32, device="cuda")
+    M.generate(x, seed, 2, 0, 0.5)
+    pool = M.MPIAsyncPool(n)
+    isend = torch.zeros(n * cols, dtype=torch.float32, device="cuda")
+    recv = torch.zeros(n * cols, dtype=torch.float32, device="cuda")
+    irecv = torch.zeros_like(recv)
+    M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=n)
+    got = recv.view(n, cols).double()
+    x64 = x.double()
+    for i in range(n):
+        Ai = A[i * per:(i + 1) * per].double()
+        g = Ai.t() @ (Ai @ x64 - b[i * per:(i + 1) * per].double())
+        err = (torch.linalg.norm(got[i] - g) / torch.linalg.norm(g)).item()
+        assert err <= 1e-5, (i, err)
+        del Ai
+    # isendbuf holds n copies of x (the reference's isendbufs[i] .= sendbuf, :130)
+    assert torch.equal(isend.view(n, cols), x.expand(n, cols))
