@@ -93,6 +93,12 @@ typedef int (*mpa_nwait_fn)(void* ctx, int64_t epoch, const int64_t* repochs, in
 
 int mpa_abi_version(void);
 const char* mpa_last_error(void);
+/* build description: target arch and the least-squares kernel variant in use */
+const char* mpa_build_info(void);
+/* tuning knobs for measurement: "lsq_variant" (index of the compiled fp32 1024-column
+ * kernel variants, DESIGN.md §Kernel tuning), "lsq_grid" (workgroups per least-squares
+ * task for tasks registered afterwards; 0 = default) */
+int mpa_tune(const char* key, int64_t value);
 
 /* ---- pool: src/MPIAsyncPools.jl:24-46 -------------------------------------------- */
 /* ranks == NULL means ranks 1:n (src/MPIAsyncPools.jl:46). */

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <new>
+#include <string>
 
 #include "comm.hpp"
 #include "kernels.hpp"
@@ -16,6 +17,7 @@ void hip_set_stream(Comm* c, void* s);
 void* hip_get_stream(Comm* c);
 void hip_set_timing(Comm* c, bool on);
 void hip_timing(Comm* c, double out[3]);
+extern int g_lsq_grid;
 }  // namespace mpa
 
 struct mpa_pool {
@@ -64,6 +66,24 @@ extern "C" {
 
 int mpa_abi_version(void) { return MPA_ABI_VERSION; }
 const char* mpa_last_error(void) { return mpa::last_error(); }
+int mpa_tune(const char* key, int64_t value) {
+  return guarded([&] {
+    const std::string k = key ? key : "";
+    if (k == "lsq_variant") {
+      if (mpa::lsq_set_variant(int(value)) < 0) mpa::fail(MPA_ARGUMENT_ERROR, "no lsq variant %lld", (long long)value);
+    } else if (k == "lsq_grid") {
+      if (value < 0 || value > (1 << 20)) mpa::fail(MPA_ARGUMENT_ERROR, "bad lsq_grid");
+      mpa::g_lsq_grid = int(value);
+    } else {
+      mpa::fail(MPA_ARGUMENT_ERROR, "unknown tuning key '%s'", k.c_str());
+    }
+  });
+}
+
+const char* mpa_build_info(void) {
+  static std::string info = std::string("gfx950; lsq c2 variant: ") + mpa::lsq_variant_name();
+  return info.c_str();
+}
 
 int mpa_pool_create(int64_t n, const int64_t* ranks, int64_t epoch0, int64_t nwait, mpa_pool** out) {
   return guarded([&] {

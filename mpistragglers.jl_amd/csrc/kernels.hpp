@@ -59,6 +59,8 @@ struct LsqBatch {
 };
 // Returns hipErrorInvalidValue if no kernel variant covers (dtype, cols).
 hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s);
+const char* lsq_variant_name();  // the c2-shape kernel variant in use (MPA_LSQ_VARIANT)
+int lsq_set_variant(int i);      // returns the number of variants, or -1 if i is out of range
 // Shape helpers for the launcher's variant table.
 int lsq_cols_pad(int dtype, int cols);  // 0 if unsupported
 int lsq_reducers(int dtype, int cols);

@@ -1,0 +1,431 @@
+// lsq_grad_kernel: the worker compute of the BASELINE workload, g_i = A_i^T (A_i x - b_i),
+// placed in the reference's compute slot (examples/iterative_example.jl:74 sleeps there).
+//
+// ONE pass over A (the single-pass requirement of SURVEY.md §7): a wave owns whole rows;
+// lane l holds the 16-B vectors v*64 + l (v < VPL) of a row, so each load instruction of
+// a wave reads 1 KiB contiguous; x and the running g stay in registers for the kernel.
+//   per row:  dot = wave_sum(sum_v a_v . x_v);  r = dot - b[row];  g_v += r * a_v
+// Rows are dealt to waves in tiles of RB rows, grid-strided so the grid sweeps one
+// contiguous region of A at a time.
+//
+// Several workers posted by the same flush run as ONE launch (LsqBatch): workgroups
+// [block0[t], block0[t+1]) serve task t.
+//
+// Cross-workgroup reduction, deterministic (no float atomics): the 4 waves of a
+// workgroup add their g in LDS in wave order, the workgroup stores its partial into
+// slab[block][:], and takes a ticket on a monotonic arrival counter.  The last R arrivers
+// (R = 4*VPL) each wait until the counter reaches the grid, then sum one 256-B column block
+// of the slab over all workgroups in block order into the reply chunk; the last of them
+// publishes completion.  Every in-kernel wait is bounded (spin_ticks).
+//
+// Compile-time variants (MODE bits) exist for measurement (DESIGN.md §Kernel tuning):
+//   M_CLAMP     branch-free loads: out-of-range rows/vectors read a clamped in-bounds
+//               address and are multiplied by zero instead of branched around
+//   M_DPP       wave reduction by DPP row ops + readlane instead of ds_bpermute
+//   M_PREFETCH  register double buffer: the next tile's loads issue before this tile's math
+//   M_NT        non-temporal loads of A (streamed once)
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "mpiasyncpools.h"
+
+namespace mpa {
+namespace {
+
+using namespace dev;
+
+enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8 };
+
+template <typename T>
+struct VecOf;
+template <>
+struct VecOf<float> {
+  typedef float type __attribute__((ext_vector_type(4)));
+};
+template <>
+struct VecOf<double> {
+  typedef double type __attribute__((ext_vector_type(2)));
+};
+
+template <typename T, bool NT>
+__device__ __forceinline__ Pack<T> ld16(const Pack<T>* p) {
+  using V = typename VecOf<T>::type;
+  V v;
+  if constexpr (NT) v = __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+  else v = *reinterpret_cast<const V*>(p);
+  Pack<T> r;
+#pragma unroll
+  for (int e = 0; e < Pack<T>::E; ++e) r.v[e] = v[e];
+  return r;
+}
+
+// DPP lane move with zero for lanes whose source is out of the row / masked row
+template <int CTRL, int RMASK>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, RMASK, 0xF, false));
+}
+template <int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const long long u = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(u), CTRL, RMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(u >> 32), CTRL, RMASK, 0xF, false);
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+__device__ __forceinline__ float dpp_add_f32(float v) {
+  // 64-lane sum: quad_perm [1,0,3,2], [2,3,0,1], row_shr 4, row_shr 8 (row totals in lanes
+  // 12-15 of each row), row_bcast 15 (rows 1,3), row_bcast 31 (rows 2,3): lane 63 = total.
+  v += dpp_f32<0xB1, 0xF>(v);
+  v += dpp_f32<0x4E, 0xF>(v);
+  v += dpp_f32<0x114, 0xF>(v);
+  v += dpp_f32<0x118, 0xF>(v);
+  v += dpp_f32<0x142, 0xA>(v);
+  v += dpp_f32<0x143, 0xC>(v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
+__device__ __forceinline__ double dpp_add_f64(double v) {
+  v += dpp_f64<0xB1, 0xF>(v);
+  v += dpp_f64<0x4E, 0xF>(v);
+  v += dpp_f64<0x114, 0xF>(v);
+  v += dpp_f64<0x118, 0xF>(v);
+  v += dpp_f64<0x142, 0xA>(v);
+  v += dpp_f64<0x143, 0xC>(v);
+  const long long u = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane(int(u), 63);
+  const int hi = __builtin_amdgcn_readlane(int(u >> 32), 63);
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+template <typename T, bool DPP>
+__device__ __forceinline__ T wave_sum(T v) {
+  if constexpr (DPP) {
+    if constexpr (sizeof(T) == 4) return dpp_add_f32(v);
+    else return dpp_add_f64(v);
+  } else {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+}
+
+template <typename T, int VPL, int RB, int MODE>
+struct Tile {
+  using P = Pack<T>;
+  static constexpr int E = P::E;
+  P d[RB][VPL];
+
+  // rows [base, base+RB): out-of-range rows/vectors either branch (default) or read a
+  // clamped in-bounds address (M_CLAMP) whose contribution is zeroed by x = 0 / res = 0
+  __device__ __forceinline__ void load(const T* A, int64_t base, int64_t rows, int64_t lda, int lane,
+                                       const bool (&vok)[VPL]) {
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int64_t r0 = base + rb;
+      if constexpr (MODE & M_CLAMP) {
+        const int64_t r = r0 < rows ? r0 : rows - 1;
+        const P* row = reinterpret_cast<const P*>(A + r * lda);
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) d[rb][v] = ld16<T, (MODE & M_NT) != 0>(row + (vok[v] ? v * 64 + lane : lane));
+      } else {
+        const P* row = reinterpret_cast<const P*>(A + r0 * lda);
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          if (r0 < rows && vok[v]) {
+            d[rb][v] = ld16<T, (MODE & M_NT) != 0>(row + v * 64 + lane);
+          } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) d[rb][v].v[e] = T(0);
+          }
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void compute(const T* __restrict__ bv, int64_t base, int64_t rows, const P (&xr)[VPL],
+                                          P (&g)[VPL]) const {
+    T dot[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      T s = T(0);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v)
+#pragma unroll
+        for (int e = 0; e < E; ++e) s += d[rb][v].v[e] * xr[v].v[e];
+      dot[rb] = s;
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) dot[rb] = wave_sum<T, (MODE & M_DPP) != 0>(dot[rb]);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int64_t r = base + rb;
+      const T res = (r < rows) ? dot[rb] - bv[r] : T(0);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v)
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[v].v[e] += res * d[rb][v].v[e];
+    }
+  }
+};
+
+template <typename T, int VPL, int RB, int MODE>
+__global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
+  using P = Pack<T>;
+  constexpr int E = P::E;
+  constexpr int R = 4 * VPL;            // reducers; each owns 16 vectors = 256 B of columns
+  __shared__ P red[VPL * 64];           // workgroup partial (VPL*64*E columns)
+  __shared__ P part[16][16];            // reducer phase partials
+  __shared__ unsigned s_ticket;
+
+  // which task of the batch this workgroup serves (wave-uniform scan over <= 16 entries)
+  int ti = 0;
+  while (ti + 1 < batch.ntasks && int(blockIdx.x) >= batch.block0[ti + 1]) ++ti;
+  const LsqTask& a = batch.t[ti];
+  const int blk = int(blockIdx.x) - batch.block0[ti];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const T* __restrict__ A = static_cast<const T*>(a.A);
+  const T* __restrict__ bv = static_cast<const T*>(a.b);
+  const T* __restrict__ xv = static_cast<const T*>(a.x);
+
+  P xr[VPL], g[VPL];
+  bool vok[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int c0 = (v * 64 + lane) * E;
+    vok[v] = c0 < a.cols;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xr[v].v[e] = (c0 + e < a.cols) ? xv[c0 + e] : T(0);
+      g[v].v[e] = T(0);
+    }
+  }
+
+  const int64_t rows = a.rows;
+  const int64_t step = int64_t(a.grid) * kWaves * RB;
+  int64_t base = (int64_t(blk) * kWaves + wave) * RB;
+  if constexpr (MODE & M_PREFETCH) {
+    Tile<T, VPL, RB, MODE> t0, t1;
+    if (base < rows) t0.load(A, base, rows, a.lda, lane, vok);
+    for (;;) {
+      const int64_t b1 = base + step;
+      if (base >= rows) break;
+      if (b1 < rows) t1.load(A, b1, rows, a.lda, lane, vok);
+      t0.compute(bv, base, rows, xr, g);
+      const int64_t b2 = b1 + step;
+      if (b1 >= rows) break;
+      if (b2 < rows) t0.load(A, b2, rows, a.lda, lane, vok);
+      t1.compute(bv, b1, rows, xr, g);
+      base = b2;
+    }
+  } else {
+    for (; base < rows; base += step) {
+      Tile<T, VPL, RB, MODE> t;
+      t.load(A, base, rows, a.lda, lane, vok);
+      t.compute(bv, base, rows, xr, g);
+    }
+  }
+
+  // workgroup partial, waves added in fixed order
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        P& dst = red[v * 64 + lane];
+        if (w == 0) {
+          dst = g[v];
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) dst.v[e] += g[v].v[e];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  P* slab = static_cast<P*>(a.slab) + size_t(blk) * (VPL * 64);
+  for (int j = tid; j < VPL * 64; j += kThreads) slab[j] = red[j];
+  drain_vm();
+  __syncthreads();
+
+  const unsigned G = unsigned(a.grid);
+  const unsigned base0 = unsigned((a.seq - 1ull) * G);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    drain_vm();
+    const unsigned old = __hip_atomic_fetch_add(&a.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_ticket = old - base0;
+  }
+  __syncthreads();
+  const unsigned ticket = s_ticket;
+  if (ticket + R < G) return;  // not one of the last R arrivers
+  const int k = int(ticket + R - G);  // reducer index 0..R-1
+
+  if (tid == 0) {
+    const unsigned long long t0 = rt_now();
+    while (__hip_atomic_load(&a.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base0 < G) {
+      __builtin_amdgcn_s_sleep(2);
+      if (rt_now() - t0 > batch.spin_ticks) {
+        __hip_atomic_fetch_or(batch.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    drain_vm();
+  }
+  __syncthreads();
+
+  // column block k: vectors [16k, 16k+16) of every slab row, summed over blocks in order
+  const int vv = tid & 15, ph = tid >> 4;
+  const P* src = static_cast<const P*>(a.slab) + k * 16 + vv;
+  P acc;
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc.v[e] = T(0);
+  for (unsigned b = unsigned(ph); b < G; b += 16) {
+    const P t = src[size_t(b) * (VPL * 64)];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc.v[e] += t.v[e];
+  }
+  part[ph][vv] = acc;
+  __syncthreads();
+  if (ph == 0) {
+    P s = part[0][vv];
+#pragma unroll
+    for (int q = 1; q < 16; ++q)
+#pragma unroll
+      for (int e = 0; e < E; ++e) s.v[e] += part[q][vv].v[e];
+    T* out = static_cast<T*>(a.out);
+    const int c0 = (k * 16 + vv) * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (c0 + e < a.cols) out[c0 + e] = s.v[e];
+  }
+  drain_vm();
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    drain_vm();
+    const unsigned base1 = unsigned((a.seq - 1ull) * unsigned(R));
+    const unsigned old = __hip_atomic_fetch_add(&a.ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old - base1 == unsigned(R - 1)) publish_done(a.flag, a.seq);
+  }
+}
+
+template <typename T, int VPL, int RB, int MODE>
+hipError_t go(const LsqBatch& a, hipStream_t s) {
+  const int grid = a.block0[a.ntasks];
+  if (grid <= 0) return hipSuccess;
+  hipLaunchKernelGGL((lsq_grad_kernel<T, VPL, RB, MODE>), dim3(grid), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+constexpr int vpl_for(int cols) {
+  constexpr int per = 64 * Pack<T>::E;
+  return (cols + per - 1) / per;
+}
+
+// tuning variants of the BASELINE c2 shape (fp32, 1024 columns), selectable with
+// MPA_LSQ_VARIANT=<index> for measurement; kDefaultC2 is the one shipped
+using Launch = hipError_t (*)(const LsqBatch&, hipStream_t);
+struct Variant {
+  Launch fn;
+  int rb;
+  const char* name;
+};
+constexpr Variant kC2Variants[] = {
+    {go<float, 4, 4, 0>, 4, "rb4"},
+    {go<float, 4, 4, M_CLAMP>, 4, "rb4+clamp"},
+    {go<float, 4, 4, M_CLAMP | M_DPP>, 4, "rb4+clamp+dpp"},
+    {go<float, 4, 2, M_CLAMP | M_DPP | M_PREFETCH>, 2, "rb2+clamp+dpp+prefetch"},
+    {go<float, 4, 4, M_CLAMP | M_DPP | M_PREFETCH>, 4, "rb4+clamp+dpp+prefetch"},
+    {go<float, 4, 4, M_CLAMP | M_DPP | M_NT>, 4, "rb4+clamp+dpp+nt"},
+    {go<float, 4, 2, M_CLAMP | M_DPP | M_PREFETCH | M_NT>, 2, "rb2+clamp+dpp+prefetch+nt"},
+    {go<float, 4, 8, M_CLAMP | M_DPP>, 8, "rb8+clamp+dpp"},
+    {go<float, 4, 2, M_CLAMP | M_DPP>, 2, "rb2+clamp+dpp"},
+};
+constexpr int kNumC2Variants = int(sizeof(kC2Variants) / sizeof(kC2Variants[0]));
+constexpr int kDefaultC2 = 2;
+
+int g_variant = -1;  // set by MPA_LSQ_VARIANT or mpa_tune("lsq_variant", i)
+
+int c2_variant() {
+  if (g_variant < 0) {
+    const char* e = std::getenv("MPA_LSQ_VARIANT");
+    const int i = e ? std::atoi(e) : kDefaultC2;
+    g_variant = (i >= 0 && i < kNumC2Variants) ? i : kDefaultC2;
+  }
+  return g_variant;
+}
+
+constexpr int kMode = M_CLAMP | M_DPP;  // shipped mode of the other shapes
+
+}  // namespace
+
+int lsq_cols_pad(int dtype, int cols) {
+  if (cols <= 0) return 0;
+  if (dtype == MPA_F32) {
+    const int v = vpl_for<float>(cols);
+    const int vp = v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 8 ? 8 : 0;
+    return vp * 64 * 4;
+  }
+  if (dtype == MPA_F64) {
+    const int v = vpl_for<double>(cols);
+    const int vp = v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 8 ? 8 : v <= 16 ? 16 : 0;
+    return vp * 64 * 2;
+  }
+  return 0;
+}
+
+int lsq_reducers(int dtype, int cols) {
+  const int cp = lsq_cols_pad(dtype, cols);
+  return cp ? 4 * (cp / (64 * (dtype == MPA_F64 ? 2 : 4))) : 0;
+}
+
+int lsq_rows_per_wave_iter(int dtype, int cols) {
+  const int cp = lsq_cols_pad(dtype, cols);
+  if (dtype == MPA_F32) {
+    if (cp == 1024) return kC2Variants[c2_variant()].rb;
+    return cp < 1024 ? 4 : 2;
+  }
+  return cp <= 256 ? 4 : cp <= 1024 ? 2 : 1;
+}
+
+const char* lsq_variant_name() { return kC2Variants[c2_variant()].name; }
+
+int lsq_set_variant(int i) {
+  if (i < 0 || i >= kNumC2Variants) return -1;
+  g_variant = i;
+  return kNumC2Variants;
+}
+
+hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s) {
+  const int cp = lsq_cols_pad(dtype, cols);
+  if (dtype == MPA_F32) {
+    switch (cp) {
+      case 256: return go<float, 1, 4, kMode>(a, s);
+      case 512: return go<float, 2, 4, kMode>(a, s);
+      case 1024: return kC2Variants[c2_variant()].fn(a, s);
+      case 2048: return go<float, 8, 2, kMode>(a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (dtype == MPA_F64) {
+    switch (cp) {
+      case 128: return go<double, 1, 4, kMode>(a, s);
+      case 256: return go<double, 2, 4, kMode>(a, s);
+      case 512: return go<double, 4, 2, kMode>(a, s);
+      case 1024: return go<double, 8, 2, kMode>(a, s);
+      case 2048: return go<double, 16, 1, kMode>(a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace mpa

@@ -31,6 +31,8 @@ namespace mpa {
     if (e_ != hipSuccess) fail(MPA_DEVICE_ERROR, "%s failed: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares task (0 = default)
+
 namespace {
 
 using Clock = std::chrono::steady_clock;
@@ -271,7 +273,8 @@ class HipComm final : public Comm {
     const int rpw = lsq_rows_per_wave_iter(ts.dtype, int(ts.cols));
     const int R = lsq_reducers(ts.dtype, int(ts.cols));
     int64_t want = (ts.rows + 4 * rpw - 1) / (4 * rpw);
-    int grid = int(want < grid_max_ ? want : grid_max_);
+    const int gmax = g_lsq_grid > 0 ? g_lsq_grid : grid_max_;
+    int grid = int(want < gmax ? want : gmax);
     if (grid < R) grid = R;
     const size_t bytes = size_t(grid) * size_t(cp) * size_t(es);
     if (bytes > w.slab_bytes) {

@@ -26,6 +26,8 @@ _sz = C.c_size_t
 SIGNATURES = [
     ("mpa_abi_version", C.c_int, []),
     ("mpa_last_error", C.c_char_p, []),
+    ("mpa_build_info", C.c_char_p, []),
+    ("mpa_tune", C.c_int, [C.c_char_p, C.c_int64]),
     ("mpa_pool_create", C.c_int, [C.c_int64, _vp, C.c_int64, C.c_int64, C.POINTER(_vp)]),
     ("mpa_pool_destroy", None, [_vp]),
     ("mpa_pool_size", C.c_int64, [_vp]),
@@ -67,6 +69,14 @@ def lib():
     """Load libmpiasyncpools.so (raises if it has not been built)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64 (soname
+        # libamdhip64.so.7, NEEDED unversioned by torch), so load torch first and let
+        # libmpiasyncpools bind to the runtime already mapped; loading ours first would map
+        # /opt/rocm's copy and torch would then map a second, disjoint runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} is missing: build the HIP library first "
