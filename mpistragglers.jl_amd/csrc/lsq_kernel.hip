@@ -282,16 +282,38 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
 
   // column block k: vectors [16k, 16k+16) of every slab row, summed over blocks in order
   const int vv = tid & 15, ph = tid >> 4;
+  // four independent accumulators keep four slab loads in flight per thread (the sum is
+  // latency-bound otherwise); combined in a fixed order, so the result is still bitwise
+  // reproducible for a given grid
   const P* src = static_cast<const P*>(a.slab) + k * 16 + vv;
-  P acc;
+  constexpr size_t S = VPL * 64;
+  P acc[4];
 #pragma unroll
-  for (int e = 0; e < E; ++e) acc.v[e] = T(0);
-  for (unsigned b = unsigned(ph); b < G; b += 16) {
-    const P t = src[size_t(b) * (VPL * 64)];
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int e = 0; e < E; ++e) acc.v[e] += t.v[e];
+    for (int e = 0; e < E; ++e) acc[q].v[e] = T(0);
+  unsigned b = unsigned(ph);
+  for (; b + 48 < G; b += 64) {
+    P t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = src[size_t(b + 16 * q) * S];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[q].v[e] += t[q].v[e];
   }
-  part[ph][vv] = acc;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    if (b < G) {
+      const P t = src[size_t(b) * S];
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[q].v[e] += t.v[e];
+      b += 16;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[0].v[e] = (acc[0].v[e] + acc[1].v[e]) + (acc[2].v[e] + acc[3].v[e]);
+  part[ph][vv] = acc[0];
   __syncthreads();
   if (ph == 0) {
     P s = part[0][vv];

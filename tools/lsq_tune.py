@@ -29,7 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--epochs", type=int, default=20)
-    ap.add_argument("--grids", default="256,512,1024,2048")
+    ap.add_argument("--grids", default="64,128,256,512")
     ap.add_argument("--variants", default="")
     a = ap.parse_args()
     n, rows, cols = 8, 1 << 20, 1024
@@ -54,6 +54,15 @@ def main():
     torch.cuda.synchronize()
     print(json.dumps({"ref": "torch.sum over A", "GBps": round(A.numel() * 4 * 10 / (s0.elapsed_time(s1) / 1e3) / 1e9, 1)}),
           flush=True)
+    for _ in range(3):
+        torch.mv(A, x)
+    s0.record()
+    for _ in range(10):
+        torch.mv(A, x)
+    s1.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"ref": "torch.mv(A, x) (vendor GEMV, A read once)",
+                      "GBps": round(A.numel() * 4 * 10 / (s0.elapsed_time(s1) / 1e3) / 1e9, 1)}), flush=True)
     nvar = 0
     while lib().mpa_tune(b"lsq_variant", nvar) == 0:
         nvar += 1
@@ -83,7 +92,7 @@ def main():
                 el = time.perf_counter() - t0
                 launches, ms, by = comm.timing()
                 comm.set_timing(False)
-                print(json.dumps({"round": rnd, "variant": v, "name": lib().mpa_build_info().decode().split(": ")[-1],
+                print(json.dumps({"round": rnd, "variant": v,
                                   "grid": g, "kernel_GBps": round(by / (ms / 1e3) / 1e9, 1),
                                   "kernel_ms": round(ms / launches, 4), "epoch_ms": round(el / a.epochs * 1e3, 4),
                                   "rel_err": err}), flush=True)
