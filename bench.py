@@ -1,17 +1,21 @@
 """Benchmark of the asyncmap! hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-One step = one coordinator epoch of the least-squares example (BASELINE configs[1], "c2"):
-    repochs = asyncmap!(pool, x, recvbuf, isendbuf, irecvbuf, comm; nwait=k)
+One step = one coordinator epoch of the least-squares example on BASELINE configs[1] ("c2"):
+    repochs = asyncmap!(pool, x, recvbuf, isendbuf, irecvbuf, comm; nwait=8)
     x -= eta * (n / #fresh) * sum_{repochs[i]==epoch} g_i          (device kernel)
-with 8 logical stream-workers, A 2^20 x 1024 fp32 row-sharded (512 MiB per worker),
-nwait = 8.  Inputs are generated on the device (Philox) and resident in
-HBM before the timed region.  `value` is iterations/sec of the whole job.
+with 8 logical workers, A 2^20 x 1024 fp32 row-sharded (512 MiB per worker).  At N = 1 the
+8 workers are stream-workers of one GPU; at N > 1 the same 8 workers (same global problem:
+strong scaling) are placed 8/N per GPU, one process per GPU, rank 0 coordinating through
+shared-memory mailboxes.  Inputs are generated on the device
+(Philox) and resident in HBM before the timed region.  `value` is
+iterations/sec of the whole job (K / max over ranks of the timed region).
 
-Rank 0 prints one JSON line with the roofline of the dominant kernel (lsq_grad_kernel,
-HIP events on the stream it runs on) and the CPU baseline (oracle/cpu_baseline: the C
-restatement of the reference's coordinator + worker threads, a bounded sample).
+Rank 0 prints one JSON line with the roofline of the dominant kernel (lsq_grad_kernel, HIP
+events on the stream it runs on, all ranks) and, at N = 1, the CPU baseline
+(oracle/cpu_baseline: the C restatement of the reference's coordinator + worker threads).
 """
 import argparse
 import json
@@ -19,8 +23,7 @@ import os
 import subprocess
 import sys
 import time
-
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # one HSA queue per stream
+import uuid
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpistragglers.jl_amd"))
@@ -28,19 +31,20 @@ sys.path.insert(0, os.path.join(ROOT, "mpistragglers.jl_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "iterations/sec + shard-kernel HBM GB/s (% peak), nwait=k of 1/2/4/8 GPUs"
 
 CONFIGS = {
-    # name: rows (global), cols, workers, nwait, dtype
     "c2": dict(rows=1 << 20, cols=1024, workers=8, nwait=8, dtype="f32",
-               desc="1xMI355X, 8 logical stream-workers, fp32 least squares A 2^20x1024 row-sharded, nwait=8"),
+               desc="BASELINE configs[1]: fp32 least squares A 2^20x1024 row-sharded over 8 logical workers, "
+                    "nwait=8 (no stragglers); 1 GPU = 8 stream-workers, N GPUs = 8/N workers per GPU"),
 }
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=300)
+    p.add_argument("--warmup", type=int, default=30)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
@@ -54,8 +58,8 @@ def cpu_baseline(cfg, seconds):
     if not os.path.exists(exe):
         try:
             subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"])
-        except Exception:
-            return None
+        except Exception as e:
+            return {"value": None, "unit": "iterations/s", "error": f"build failed: {e}"[:200]}
     cmd = [exe, "--workers", str(cfg["workers"]), "--rows", str(cfg["rows"]), "--cols", str(cfg["cols"]),
            "--nwait", str(cfg["nwait"]), "--seconds", str(seconds)]
     try:
@@ -65,45 +69,84 @@ def cpu_baseline(cfg, seconds):
         return {"value": None, "unit": "iterations/s", "error": str(e)[:200]}
     return {"value": round(r["it_per_s"], 4), "unit": "iterations/s", "cores": r["threads"], "kind": "port",
             "sample": f"{r['epochs']} epochs in {r['seconds']:.1f} s of the full {cfg['config']} problem "
-                      f"({r['workers']} worker threads + 1 coordinator thread, fp32, AVX2 loops); "
-                      f"{r['alg_GBps']:.1f} GB/s algorithmic"}
+                      f"({r['workers']} worker threads + 1 coordinator thread, fp32, AVX2 loops, same state "
+                      f"machine); {r['alg_GBps']:.1f} GB/s algorithmic"}
 
 
-def main():
-    args = parse()
-    cfg = dict(CONFIGS[args.config])
-    cfg["config"] = args.config
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if world > 1:
-        import multigpu  # noqa: F401  (placed next to bench.py)
-        return multigpu.run(args, cfg, rank, world, local)
+def step_size(rows, cols):
+    """0.9 / L with L ~ ||A||^2 for U(-1,1)/sqrt(cols) entries."""
+    L = rows / (3.0 * cols) * (1.0 + np.sqrt(cols / rows)) ** 2
+    return 0.9 / L
 
+
+def gen_shard(M, torch, cfg, seed, w):
+    """Rows of worker w (1-based) of the global synthetic problem, on the current GPU."""
+    n, rows, cols = cfg["workers"], cfg["rows"], cfg["cols"]
+    per = rows // n
+    A = torch.empty(per, cols, dtype=torch.float32, device="cuda")
+    b = torch.empty(per, dtype=torch.float32, device="cuda")
+    M.generate(A, seed, 0, (w - 1) * per * cols, float(np.float32(1.0 / np.sqrt(cols))))
+    M.generate(b, seed, 1, (w - 1) * per, 1.0)
+    return A, b
+
+
+def report(args, cfg, world, el, kl, kms, kbytes, extra):
+    its = args.steps / el
+    n, rows, cols = cfg["workers"], cfg["rows"], cfg["cols"]
+    per_launch_bytes = kbytes / max(kl, 1)
+    per_launch_s = kms / 1e3 / max(kl, 1)
+    achieved = per_launch_bytes / per_launch_s / 1e9 if kl else None
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "lsq_pmc_c2.json")
+    if os.path.exists(pmc) and world == 1:
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": round(its, 3),
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Philox4x32-10 generated on device, DESIGN.md §Data)",
+        "config": {"workload": cfg["desc"], "rows": rows, "cols": cols, "workers": n, "nwait": cfg["nwait"],
+                   "shard_bytes": rows // n * cols * 4, "parallelism": f"{n} logical workers on {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
+                     "traffic": traffic,
+                     "kernel": "lsq_grad_kernel (one batched launch per epoch per GPU)",
+                     "alg_bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4),
+                     "launches": kl},
+        "epoch_alg_GBps": round(4.0 * (rows * cols + rows + 2 * n * cols) * its / 1e9, 1),
+    }
+    out.update(extra)
+    return out
+
+
+def run_single(args, cfg):
     import torch
     import mpiasyncpools as M
 
-    torch.cuda.set_device(local)
-    n, rows, cols, nwait = cfg["workers"], cfg["rows"], cfg["cols"], cfg["nwait"]
-    per = rows // n
-    tdt = torch.float32
-    es = 4
-    A = torch.empty(rows, cols, dtype=tdt, device="cuda")
-    b = torch.empty(rows, dtype=tdt, device="cuda")
-    M.generate(A, args.seed, 0, 0, float(np.float32(1.0 / np.sqrt(cols))))
-    M.generate(b, args.seed, 1, 0, 1.0)
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    n, cols, nwait = cfg["workers"], cfg["cols"], cfg["nwait"]
     comm = M.DeviceComm(n)
-    for r in range(1, n + 1):
-        comm.set_task_lsq(r, A[(r - 1) * per:r * per], b[(r - 1) * per:r * per])
+    shards = [gen_shard(M, torch, cfg, args.seed, w) for w in range(1, n + 1)]
+    for w, (A, b) in enumerate(shards, start=1):
+        comm.set_task_lsq(w, A, b)
     pool = M.MPIAsyncPool(n)
-    x = torch.zeros(cols, dtype=tdt, device="cuda")
-    isend = torch.zeros(n * cols, dtype=tdt, device="cuda")
-    recv = torch.zeros(n * cols, dtype=tdt, device="cuda")
+    x = torch.zeros(cols, device="cuda")
+    isend = torch.zeros(n * cols, device="cuda")
+    recv = torch.zeros(n * cols, device="cuda")
     irecv = torch.zeros_like(recv)
-    L = rows / (3.0 * cols) * (1.0 + np.sqrt(cols / rows)) ** 2
-    eta = 0.9 / L
+    eta = step_size(cfg["rows"], cols)
     w = np.zeros(n)
 
     def step():
@@ -116,63 +159,117 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    comm.timing()  # discard warmup launches
+    comm.timing()
     comm.set_timing(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    launches, kms, kbytes = comm.timing()
+    el = time.perf_counter() - t0
+    kl, kms, kbytes = comm.timing()
     comm.set_timing(False)
     M.waitall_(pool, recv, irecv)
-    el = t1 - t0
-    its = args.steps / el
-    alg_bytes_epoch = es * (rows * cols + rows + 2 * n * cols)
-    per_launch_bytes = kbytes / max(launches, 1)
-    per_launch_s = kms / 1e3 / max(launches, 1)
-    achieved = per_launch_bytes / per_launch_s / 1e9 if launches else None
-    xnorm = float(torch.linalg.norm(x).item())
+    extra = {"x_norm": float(torch.linalg.norm(x).item()), "build": M.lib().mpa_build_info().decode()}
+    extra["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(cfg, args.cpu_seconds)
+    print(json.dumps(report(args, cfg, 1, el, kl, kms, kbytes, extra)), flush=True)
 
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "lsq_pmc_c2.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
 
-    out = {
-        "metric": "iterations/sec + shard-kernel HBM GB/s (% peak), nwait=k of 1/2/4/8 GPUs",
-        "value": round(its, 3),
-        "unit": "iterations/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (Philox4x32-10 on device, DESIGN.md §Data)",
-        "config": {"workload": cfg["desc"], "rows": rows, "cols": cols, "workers": n, "nwait": nwait,
-                   "shard_bytes": per * cols * es, "parallelism": f"{n} stream-workers on {world} GPU"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                     "traffic": traffic,
-                     "kernel": "lsq_grad_kernel<float,4,4> (one batched launch per epoch)",
-                     "alg_bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4),
-                     "launches": launches},
-        "epoch_alg_GBps": round(alg_bytes_epoch * its / 1e9, 1),
-        "x_norm": xnorm,
-    }
-    if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+def run_multi(args, cfg, rank, world, local):
+    """One process per GPU: rank 0 coordinates; every rank serves the workers placed on it."""
+    import torch
+    import torch.distributed as dist
+    import mpiasyncpools as M
+
+    # MPA_BENCH_ONE_GPU=1 rehearses the N-process path with every rank on GPU 0 (1-GPU box)
+    torch.cuda.set_device(0 if os.environ.get("MPA_BENCH_ONE_GPU") == "1" else local)
+    dist.init_process_group("gloo")
+    n, cols, nwait = cfg["workers"], cfg["cols"], cfg["nwait"]
+    placement = [(w * world) // n for w in range(n)]  # 8/N consecutive workers per rank
+    name = [f"/mpa_bench_{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+    if rank == 0:
+        comm = M.DistComm(n, placement, 0, name[0], cols * 4)
+    dist.broadcast_object_list(name, src=0)
+    if rank != 0:
+        comm = M.DistComm(n, placement, rank, name[0], cols * 4)
+    keep = []
+    for w in range(1, n + 1):
+        if placement[w - 1] == rank:
+            A, b = gen_shard(M, torch, cfg, args.seed, w)
+            keep.append((A, b))
+            comm.set_task_lsq(w, A, b)
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank == 0:
+        pool = M.MPIAsyncPool(n)
+        x = torch.zeros(cols, device="cuda")
+        isend = torch.zeros(n * cols, device="cuda")
+        recv = torch.zeros(n * cols, device="cuda")
+        irecv = torch.zeros_like(recv)
+        eta = step_size(cfg["rows"], cols)
+        wts = np.zeros(n)
+
+        def step():
+            rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=nwait)
+            fresh = rep == pool.epoch
+            nf = int(fresh.sum())
+            wts[:] = fresh * (n / nf if nf else 0.0)
+            comm.lsq_update(x, recv, n, wts, eta)
+
+        for _ in range(args.warmup):
+            step()
+        M.waitall_(pool, recv, irecv)
+        torch.cuda.synchronize()
+        comm.pause_servers()
     else:
-        out["cpu_baseline"] = None
-    print(json.dumps(out), flush=True)
+        comm.serve()  # warmup session, returns at pause_servers
+    comm.timing()
+    comm.set_timing(True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    if rank == 0:
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        M.waitall_(pool, recv, irecv)
+        comm.shutdown()
+    else:
+        comm.serve()  # timed session, returns at shutdown
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    kl, kms, kbytes = comm.timing()
+    comm.set_timing(False)
+    dist.barrier()
+    stats = [None] * world
+    dist.all_gather_object(stats, (el, kl, kms, kbytes))
+    if rank == 0:
+        el_max = max(s[0] for s in stats)
+        kl = sum(s[1] for s in stats)
+        kms = sum(s[2] for s in stats)
+        kbytes = sum(s[3] for s in stats)
+        extra = {"x_norm": float(torch.linalg.norm(x).item()), "build": M.lib().mpa_build_info().decode(),
+                 "placement": placement, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None}
+        print(json.dumps(report(args, cfg, world, el_max, kl, kms, kbytes, extra)), flush=True)
+    dist.barrier()
+    comm.close()
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    cfg = dict(CONFIGS[args.config])
+    cfg["config"] = args.config
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (launch N > 1 with torch.distributed.run)")
+    if world == 1:
+        run_single(args, cfg)
+    else:
+        run_multi(args, cfg, rank, world, local)
 
 
 if __name__ == "__main__":

@@ -74,6 +74,8 @@ enum mpa_dtype { MPA_F32 = 0, MPA_F64 = 1, MPA_BF16 = 2 };
 enum mpa_transport {
   MPA_TRANSPORT_HIP = 0, /* the product: device workers on HIP streams */
   MPA_TRANSPORT_SIM = 1, /* deterministic virtual-clock host transport, for host-logic tests */
+  MPA_TRANSPORT_HOST = 2, /* multi-process mailbox protocol with host-executed test workers,
+                             for tests of the N > 1 control plane without a GPU */
 };
 
 enum mpa_nwait_kind { MPA_NWAIT_INT = 0, MPA_NWAIT_FN = 1, MPA_NWAIT_OTHER = 2 };
@@ -157,6 +159,21 @@ int mpa_comm_set_delays(mpa_comm* comm, int64_t rank, const int64_t* delays_ns, 
 int64_t mpa_comm_tasks_done(mpa_comm* comm, int64_t rank);
 /* control channel: wait for every outstanding task, then refuse further posts */
 int mpa_comm_shutdown(mpa_comm* comm);
+/* ---- multi-process communicators: one process per GPU ------- */
+/* placement[w] = the process rank that serves worker w+1 (rank 0 is the coordinator's own
+ * process).  my_rank 0 creates the shared-memory mailboxes `shm_name` (POSIX shm name,
+ * messages of at most max_msg_bytes each way), every other rank attaches to them after
+ * rank 0 has created them.  On rank 0 the comm is used with mpa_asyncmap/mpa_waitall; on
+ * the other ranks, after registering the tasks of their workers, with mpa_comm_serve.
+ * transport: MPA_TRANSPORT_HIP (the product) or MPA_TRANSPORT_HOST (protocol tests). */
+int mpa_comm_create_dist(int transport, int64_t nworkers, const int* placement, int my_rank,
+                         const char* shm_name, size_t max_msg_bytes, mpa_comm** out);
+/* worker processes: run the tasks posted to the workers placed on this rank (the
+ * reference's worker_main loop, examples/iterative_example.jl:55-82) until rank 0 pauses
+ * the servers or shuts the comm down */
+int mpa_comm_serve(mpa_comm* comm);
+/* rank 0: make every running mpa_comm_serve return (e.g. around a barrier) */
+int mpa_comm_pause_servers(mpa_comm* comm);
 /* HIP transport: time every worker-task kernel launch with HIP events on the stream it
  * runs on (enable = 1 / 0).  mpa_comm_timing returns, since its previous call:
  * out[0] launches, out[1] summed kernel milliseconds, out[2] summed algorithmic bytes

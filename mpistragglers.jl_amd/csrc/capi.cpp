@@ -18,6 +18,12 @@ void* hip_get_stream(Comm* c);
 void hip_set_timing(Comm* c, bool on);
 void hip_timing(Comm* c, double out[3]);
 extern int g_lsq_grid;
+Comm* make_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg);
+void hip_serve(Comm* c);
+void hip_pause_servers(Comm* c);
+Comm* make_host_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg);
+void host_serve(Comm* c);
+void host_pause_servers(Comm* c);
 }  // namespace mpa
 
 struct mpa_pool {
@@ -137,6 +143,37 @@ int mpa_comm_create(int transport, int64_t nworkers, const int* devices, mpa_com
     else if (transport == MPA_TRANSPORT_SIM) c = mpa::make_sim_comm(nworkers);
     else mpa::fail(MPA_ARGUMENT_ERROR, "unknown transport %d", transport);
     *out = new mpa_comm{c};
+  });
+}
+
+int mpa_comm_create_dist(int transport, int64_t nworkers, const int* placement, int my_rank, const char* shm_name,
+                         size_t max_msg_bytes, mpa_comm** out) {
+  return guarded([&] {
+    if (!out) mpa::fail(MPA_ARGUMENT_ERROR, "out is NULL");
+    if (nworkers < 0 || my_rank < 0) mpa::fail(MPA_ARGUMENT_ERROR, "bad nworkers / rank");
+    mpa::Comm* c = nullptr;
+    if (transport == MPA_TRANSPORT_HIP) c = mpa::make_dist_comm(nworkers, placement, my_rank, shm_name, max_msg_bytes);
+    else if (transport == MPA_TRANSPORT_HOST) c = mpa::make_host_dist_comm(nworkers, placement, my_rank, shm_name, max_msg_bytes);
+    else mpa::fail(MPA_ARGUMENT_ERROR, "multi-process communicators are MPA_TRANSPORT_HIP or MPA_TRANSPORT_HOST");
+    *out = new mpa_comm{c};
+  });
+}
+
+int mpa_comm_serve(mpa_comm* comm) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    if (c.transport() == MPA_TRANSPORT_HIP) mpa::hip_serve(&c);
+    else if (c.transport() == MPA_TRANSPORT_HOST) mpa::host_serve(&c);
+    else mpa::fail(MPA_ARGUMENT_ERROR, "not a multi-process communicator");
+  });
+}
+
+int mpa_comm_pause_servers(mpa_comm* comm) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    if (c.transport() == MPA_TRANSPORT_HIP) mpa::hip_pause_servers(&c);
+    else if (c.transport() == MPA_TRANSPORT_HOST) mpa::host_pause_servers(&c);
+    else mpa::fail(MPA_ARGUMENT_ERROR, "not a multi-process communicator");
   });
 }
 

@@ -38,21 +38,32 @@ __device__ void block_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
 
 __global__ void __launch_bounds__(kThreads) exchange_kernel(ExchangeArgs a) {
   const int b = blockIdx.x;
-  const int npb = a.npost * a.bpp;
-  if (b < npb) {
-    const int item = b / a.bpp, part = b % a.bpp;
-    const uint64_t off = uint64_t(part) * a.ppart;
-    if (off >= a.sl) return;
-    const uint64_t len = (a.sl - off) < a.ppart ? (a.sl - off) : a.ppart;
-    block_copy(a.isendbuf + uint64_t(a.post[item]) * a.sl + off, a.sendbuf + off, len);
-  } else {
-    const int hb = b - npb;
-    const int item = hb / a.bph, part = hb % a.bph;
-    const uint64_t off = uint64_t(part) * a.hpart;
-    if (off >= a.rl) return;
-    const uint64_t len = (a.rl - off) < a.hpart ? (a.rl - off) : a.hpart;
-    const uint64_t c = uint64_t(a.harv[item]) * a.rl + off;
-    block_copy(a.recvbuf + c, a.irecvbuf + c, len);
+  int i = 0;  // copy item of this block (uniform scan)
+  while (i + 1 < a.ncopy && b >= a.block0[i + 1]) ++i;
+  if (a.ncopy > 0) {
+    const CopyItem& c = a.c[i];
+    const uint64_t off = uint64_t(b - a.block0[i]) * a.part;
+    if (off < c.bytes) {
+      const uint64_t len = (c.bytes - off) < a.part ? (c.bytes - off) : a.part;
+      block_copy(c.dst + off, c.src + off, len);
+    }
+  }
+  if (a.ndoor == 0) return;
+  // every block's copies drained and released at system scope (the mailboxes are host
+  // memory read by another GPU), then the last block to arrive rings the doorbells
+  __shared__ unsigned s_last;
+  drain_vm();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    drain_vm();
+    const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old - a.ticket_base) == gridDim.x - 1;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (int d = 0; d < a.ndoor; ++d)
+        __hip_atomic_store(a.door[d], a.doorval[d], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -144,7 +155,8 @@ __global__ void __launch_bounds__(kThreads) generate_kernel(void* out, int dtype
 }  // namespace
 
 hipError_t launch_exchange(const ExchangeArgs& a, hipStream_t s) {
-  const int grid = a.npost * a.bpp + a.nharv * a.bph;
+  int grid = a.block0[a.ncopy];
+  if (grid == 0 && a.ndoor > 0) grid = 1;  // doorbells only
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(exchange_kernel, dim3(grid), dim3(kThreads), 0, s, a);
   return hipGetLastError();

@@ -8,20 +8,26 @@
 
 namespace mpa {
 
-constexpr int kMaxExchangeItems = 64;
-
+// One flush of the pool = ONE exchange launch: a list of byte copies (sendbuf -> isendbuf
+// slots, sendbuf -> remote workers' mailboxes, irecvbuf/mailbox replies -> recvbuf
+// chunks) and, once every copy of the launch is complete and released at system scope,
+// the doorbells of the remote workers it posted to (rung by the last block to finish).
+constexpr int kMaxCopies = 48;
+constexpr int kMaxDoorbells = 16;
+struct CopyItem {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint64_t bytes;
+};
 struct ExchangeArgs {
-  const uint8_t* sendbuf;
-  uint8_t* isendbuf;
-  uint64_t sl;
-  uint8_t* recvbuf;
-  const uint8_t* irecvbuf;
-  uint64_t rl;
-  int npost, nharv;
-  int bpp, bph;      // blocks per post item / per harvest item
-  uint64_t ppart, hpart;  // bytes per block (multiple of 16)
-  int16_t post[kMaxExchangeItems];
-  int16_t harv[kMaxExchangeItems];
+  int ncopy, ndoor;
+  uint64_t part;  // bytes per block (multiple of 16)
+  int block0[kMaxCopies + 1];
+  CopyItem c[kMaxCopies];
+  unsigned long long* door[kMaxDoorbells];
+  unsigned long long doorval[kMaxDoorbells];
+  uint32_t* ticket;      // monotonic block counter in device memory (doorbell launches only)
+  uint32_t ticket_base;  // its value before this launch
 };
 hipError_t launch_exchange(const ExchangeArgs& a, hipStream_t s);
 

@@ -372,7 +372,7 @@ constexpr Variant kC2Variants[] = {
     {go<float, 4, 2, M_CLAMP | M_DPP>, 2, "rb2+clamp+dpp"},
 };
 constexpr int kNumC2Variants = int(sizeof(kC2Variants) / sizeof(kC2Variants[0]));
-constexpr int kDefaultC2 = 2;
+constexpr int kDefaultC2 = 5;  // rb4+clamp+dpp+nt: 6.5 TB/s on c2 (profiles/r01_tune.txt)
 
 int g_variant = -1;  // set by MPA_LSQ_VARIANT or mpa_tune("lsq_variant", i)
 
@@ -385,7 +385,7 @@ int c2_variant() {
   return g_variant;
 }
 
-constexpr int kMode = M_CLAMP | M_DPP;  // shipped mode of the other shapes
+constexpr int kMode = M_CLAMP | M_DPP | M_NT;  // shipped mode of the other shapes
 
 }  // namespace
 

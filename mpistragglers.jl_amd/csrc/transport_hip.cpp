@@ -2,26 +2,39 @@
 //
 //   MPI.Isend(isendbufs[i]) + MPI.Irecv!(irecvbufs[i])   (src/MPIAsyncPools.jl:137-138)
 //     -> post(): deferred to flush(), where ONE exchange kernel on the coordinator stream
-//        copies sendbuf into every posted slot of isendbuf (and performs the pending
-//        harvest copies), one event is recorded, and each posted worker's stream waits
-//        on it and runs [delay kernel] + task kernel.  The task kernel reads x from its
-//        isendbuf slot and writes its reply into its irecvbuf chunk.
+//        copies sendbuf into every posted slot of isendbuf (and into the mailbox of every
+//        worker served by another process, whose doorbell the same kernel rings once its
+//        copies are released), performs the pending harvest copies, and one event orders
+//        the task launches of the workers served here after it.
 //   MPI.Test! / MPI.Waitany! / MPI.Waitall!               (:99, :161, :212)
-//     -> loads of the worker's host-pinned completion word, which the task kernel's last
+//     -> loads of the worker's host-visible completion word, which the task kernel's last
 //        workgroup publishes with a system-scope release (no hipEventQuery, no sync call).
 //   recvbufs[i] .= irecvbufs[i]                          (:108, :167, :216)
 //     -> deferred and batched into the next exchange kernel on the coordinator stream,
 //        which is ordered before any later re-post to that worker (the reference's
 //        program order, :167 before :182-183).
+//
+// Roles.  SOLO: one process, every worker on this GPU.  COORD: rank 0 of a multi-process
+// communicator (one process per GPU); workers placed on rank 0 run
+// here, the others are reached through shared-memory mailboxes (shm.hpp).  SERVER: a
+// worker process; serve() watches the doorbells of its workers and launches their tasks,
+// whose replies and completion words land in the mailboxes.
+//
+// Streams.  Every worker stream and launch stream is CU-masked with every CU enabled:
+// such a stream gets an HSA queue of its own, whereas plain streams beyond
+// GPU_MAX_HW_QUEUES share queues and HIP serialises kernels of a shared queue
+// (profiles/r01_hw_queues.txt), which would let one straggler hold back another worker.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
-#include <thread>
+#include <memory>
 
 #include "comm.hpp"
 #include "kernels.hpp"
+#include "shm.hpp"
 
 namespace mpa {
 
@@ -31,55 +44,159 @@ namespace mpa {
     if (e_ != hipSuccess) fail(MPA_DEVICE_ERROR, "%s failed: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
-int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares task (0 = default)
+int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares launch (0 = default)
 
 namespace {
 
 using Clock = std::chrono::steady_clock;
+constexpr int kDefaultLaunchGrid = 512;  // 2 workgroups per CU: profiles/r01_tune_sweep2.jsonl
+constexpr int kSlabGridCap = 1024;       // most workgroups a single task may be given
+constexpr int kLaunchStreams = 2;
+
+hipStream_t make_queue_stream(int device) {
+  hipDeviceProp_t p;
+  HIPCHECK(hipGetDeviceProperties(&p, device));
+  const int cus = p.multiProcessorCount;
+  std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0xFFFFFFFFu);
+  if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+  hipStream_t s = nullptr;
+  HIPCHECK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+  return s;
+}
 
 struct HipWorker {
-  int device = 0;
+  bool here = true;     // its tasks run in this process
+  bool remote = false;  // coordinator's view of a worker served by another process
   hipStream_t stream = nullptr;
-  unsigned long long seq = 0;  // tasks posted
-  // LSQ resources
+  unsigned long long seq = 0;  // coordinator: tasks posted; server: tasks served
   void* slab = nullptr;
-  size_t slab_bytes = 0;
-  int grid = 0;
-  // per-post pointers
+  int slab_grid = 0;
+  // current task
   int64_t slot = -1;
   const uint8_t* x = nullptr;
   uint8_t* out = nullptr;
   size_t sl = 0, rl = 0;
+  unsigned long long* flag_host = nullptr;  // completion word, host view
+  unsigned long long* flag_dev = nullptr;   // the same word, device view
+  // mailbox (remote worker on the coordinator / served worker in a worker process)
+  BoxHeader* box = nullptr;
+  uint8_t* box_msg_dev = nullptr;
+  uint8_t* box_reply_dev = nullptr;
+  unsigned long long* box_door_dev = nullptr;
+  uint8_t* xslot = nullptr;  // server: device copy of the staged message
+};
+
+// Accumulates copy items and doorbells into as few exchange launches as fit the kernel
+// argument (kMaxCopies / kMaxDoorbells per launch), in order.
+class ExchangeBuilder {
+ public:
+  ExchangeBuilder(uint32_t* ticket, uint32_t* ticket_count, hipStream_t s)
+      : ticket_(ticket), count_(ticket_count), s_(s) {
+    reset();
+  }
+  void reserve(int copies, int doors) {
+    if (a_.ncopy + copies > kMaxCopies || a_.ndoor + doors > kMaxDoorbells) launch();
+  }
+  void copy(const uint8_t* src, uint8_t* dst, uint64_t bytes) {
+    if (bytes == 0) return;
+    reserve(1, 0);
+    CopyItem& c = a_.c[a_.ncopy];
+    c.src = src;
+    c.dst = dst;
+    c.bytes = bytes;
+    a_.block0[a_.ncopy] = blocks_;
+    blocks_ += int((bytes + kPart - 1) / kPart);
+    a_.ncopy += 1;
+    a_.block0[a_.ncopy] = blocks_;
+  }
+  void door(unsigned long long* addr, unsigned long long value) {
+    reserve(0, 1);
+    a_.door[a_.ndoor] = addr;
+    a_.doorval[a_.ndoor] = value;
+    a_.ndoor += 1;
+  }
+  void launch() {
+    if (a_.ncopy == 0 && a_.ndoor == 0) return;
+    const int grid = blocks_ > 0 ? blocks_ : 1;
+    if (a_.ndoor > 0) {
+      a_.ticket = ticket_;
+      a_.ticket_base = *count_;
+      *count_ += uint32_t(grid);
+    }
+    HIPCHECK(launch_exchange(a_, s_));
+    reset();
+  }
+
+ private:
+  static constexpr uint64_t kPart = 64 * 1024;
+  void reset() {
+    a_ = ExchangeArgs{};
+    a_.part = kPart;
+    blocks_ = 0;
+  }
+  ExchangeArgs a_{};
+  int blocks_ = 0;
+  uint32_t* ticket_;
+  uint32_t* count_;
+  hipStream_t s_;
 };
 
 class HipComm final : public Comm {
  public:
-  HipComm(int64_t n, const int* devices) : Comm(n), w_(size_t(n)) {
+  enum Role { SOLO, COORD, SERVER };
+
+  HipComm(int64_t n, const int* devices, const int* placement, int my_rank, ShmRegion* region)
+      : Comm(n), w_(size_t(n)), region_(region), my_rank_(my_rank) {
+    role_ = !region ? SOLO : my_rank == 0 ? COORD : SERVER;
     HIPCHECK(hipGetDevice(&dev_));
     for (int64_t i = 0; i < n; ++i) {
-      w_[size_t(i)].device = devices ? devices[i] : dev_;
-      if (w_[size_t(i)].device != dev_)
-        fail(MPA_ARGUMENT_ERROR, "worker %lld on device %d: workers on other devices than the coordinator's (%d) "
-             "are served by per-device worker processes (DESIGN.md §Multi-GPU)", (long long)(i + 1),
-             w_[size_t(i)].device, dev_);
+      HipWorker& w = w_[size_t(i)];
+      const int host_rank = placement ? placement[i] : 0;
+      w.here = host_rank == my_rank_;
+      w.remote = role_ == COORD && !w.here;
+      if (devices && w.here && devices[i] != dev_)
+        fail(MPA_ARGUMENT_ERROR, "worker %lld on device %d: a process serves the workers of its own device (%d); "
+             "workers of other devices are served by their own processes (DESIGN.md §Multi-GPU)",
+             (long long)(i + 1), devices[i], dev_);
     }
-    for (auto& w : w_) HIPCHECK(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
-    launch_streams_.resize(size_t(n < 2 ? 2 : n));
-    for (auto& s : launch_streams_) HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&flags_), sizeof(unsigned long long) * size_t(n + 1),
                            hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(flags_, 0, sizeof(unsigned long long) * size_t(n + 1));
     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&err_), 64, hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(err_, 0, 64);
-    HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * 2 * size_t(n)));
-    HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * 2 * size_t(n)));
+    HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (2 * size_t(n) + 1)));
+    HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (2 * size_t(n) + 1)));
+    err_dev_ = err_;
+    if (region_) {
+      if (region_->nworkers() != n) fail(MPA_ARGUMENT_ERROR, "shared memory holds %lld workers, comm has %lld",
+                                         (long long)region_->nworkers(), (long long)n);
+      if (role_ == SERVER) err_dev_ = region_->dev(&region_->header()->err);
+    }
+    for (int64_t r = 1; r <= n; ++r) {
+      HipWorker& w = w_[size_t(r - 1)];
+      if (region_ && (w.remote || (role_ == SERVER && w.here))) {
+        w.box = region_->box(r);
+        w.box_msg_dev = region_->dev(region_->msg(r));
+        w.box_reply_dev = region_->dev(region_->reply(r));
+        w.box_door_dev = region_->dev(&w.box->doorbell);
+      }
+      if (role_ == SERVER && w.here) {
+        w.flag_host = &w.box->done;
+        w.flag_dev = region_->dev(&w.box->done);
+        HIPCHECK(hipMalloc(&w.xslot, region_->max_msg()));
+      } else if (w.remote) {
+        w.flag_host = &w.box->done;
+      } else {
+        w.flag_host = &flags_[r - 1];
+        w.flag_dev = &flags_[r - 1];
+      }
+      if (w.here) w.stream = make_queue_stream(dev_);
+    }
+    for (int k = 0; k < kLaunchStreams; ++k) launch_streams_.push_back(make_queue_stream(dev_));
     HIPCHECK(hipEventCreateWithFlags(&xfer_ev_, hipEventDisableTiming));
     int khz = 0;
     HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
     rt_hz_ = khz > 0 ? double(khz) * 1e3 : 100e6;
-    const char* g = std::getenv("MPA_LSQ_GRID");
-    grid_max_ = g ? std::atoi(g) : 512;
-    if (grid_max_ < 16) grid_max_ = 16;
     const char* t = std::getenv("MPA_WAIT_TIMEOUT_S");
     timeout_s_ = t ? std::atof(t) : 600.0;
     HIPCHECK(hipDeviceSynchronize());
@@ -89,43 +206,54 @@ class HipComm final : public Comm {
     (void)hipDeviceSynchronize();
     for (auto& w : w_) {
       if (w.slab) (void)hipFree(w.slab);
+      if (w.xslot) (void)hipFree(w.xslot);
       if (w.stream) (void)hipStreamDestroy(w.stream);
     }
     for (auto& s : launch_streams_) (void)hipStreamDestroy(s);
-    for (auto& t : timed_) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
+    for (auto& t : timed_) {
+      (void)hipEventDestroy(t.start);
+      (void)hipEventDestroy(t.stop);
+    }
     for (auto e : event_pool_) (void)hipEventDestroy(e);
     if (ctr_) (void)hipFree(ctr_);
     if (flags_) (void)hipHostFree(flags_);
     if (err_) (void)hipHostFree(err_);
     if (xfer_ev_) (void)hipEventDestroy(xfer_ev_);
+    delete region_;
   }
 
   int transport() const override { return MPA_TRANSPORT_HIP; }
   void set_stream(hipStream_t s) { coord_ = s; }
   hipStream_t stream() const { return coord_; }
-  double rt_hz() const { return rt_hz_; }
 
-  void begin_call(const CallBufs& b) override { b_ = b; }
+  void begin_call(const CallBufs& b) override {
+    if (role_ == SERVER) fail(MPA_ERROR, "asyncmap!/waitall! run on rank 0; this process serves workers (mpa_comm_serve)");
+    b_ = b;
+  }
 
   void post(int64_t i, int64_t rank, int64_t tag) override {
     (void)tag;
     if (shutdown_) fail(MPA_ERROR, "comm has been shut down");
     HipWorker& w = w_[size_t(rank - 1)];
-    const TaskSpec& ts = tasks_[size_t(rank - 1)];
-    check_task(rank, ts, b_.sl, b_.rl);
+    if (w.remote) {
+      if (b_.sl > region_->max_msg() || b_.rl > region_->max_msg())
+        fail(MPA_DIMENSION_MISMATCH, "messages of %zu / %zu bytes exceed the communicator's mailbox of %zu bytes",
+             b_.sl, b_.rl, region_->max_msg());
+      w.box->msg_bytes = b_.sl;
+      w.box->reply_bytes = b_.rl;
+    } else {
+      check_task(rank, tasks_[size_t(rank - 1)], b_.sl, b_.rl);
+      w.x = b_.isendbuf + size_t(i) * b_.sl;
+      w.out = b_.irecvbuf + size_t(i) * b_.rl;
+    }
     w.slot = i;
-    w.x = b_.isendbuf + size_t(i) * b_.sl;
-    w.out = b_.irecvbuf + size_t(i) * b_.rl;
     w.sl = b_.sl;
     w.rl = b_.rl;
     w.seq += 1;
     posts_.push_back(rank);
   }
 
-  void harvest(int64_t i, int64_t rank) override {
-    (void)rank;
-    harv_.push_back(i);
-  }
+  void harvest(int64_t i, int64_t rank) override { harv_.push_back({i, rank}); }
 
   bool test(int64_t i, int64_t rank) override {
     (void)i;
@@ -159,32 +287,37 @@ class HipComm final : public Comm {
   void flush() override {
     if (posts_.empty() && harv_.empty()) return;
     if (timing_) reap_timing(false);
-    // the reference copies at dispatch/harvest time (:108, :130); here one kernel per flush
-    size_t p = 0, h = 0;
-    while (p < posts_.size() || h < harv_.size()) {
-      ExchangeArgs ea{};
-      ea.sendbuf = b_.sendbuf;
-      ea.isendbuf = b_.isendbuf;
-      ea.sl = b_.sl;
-      ea.recvbuf = b_.recvbuf;
-      ea.irecvbuf = b_.irecvbuf;
-      ea.rl = b_.rl;
-      for (; p < posts_.size() && ea.npost < kMaxExchangeItems; ++p)
-        ea.post[ea.npost++] = int16_t(w_[size_t(posts_[p] - 1)].slot);
-      for (; h < harv_.size() && ea.nharv < kMaxExchangeItems; ++h) ea.harv[ea.nharv++] = int16_t(harv_[h]);
-      constexpr uint64_t kPart = 64 * 1024;
-      ea.ppart = kPart;
-      ea.hpart = kPart;
-      ea.bpp = int((b_.sl + kPart - 1) / kPart);
-      ea.bph = int((b_.rl + kPart - 1) / kPart);
-      if (ea.bpp == 0) ea.npost = 0;
-      if (ea.bph == 0) ea.nharv = 0;
-      HIPCHECK(launch_exchange(ea, coord_));
+    ExchangeBuilder xb(ticket_, &ticket_count_, coord_);
+    // harvests first: a worker re-posted by this flush is only told to go (doorbell, or
+    // the event below) after its previous reply has been copied out
+    for (const auto& h : harv_) {
+      const HipWorker& w = w_[size_t(h.rank - 1)];
+      const uint8_t* src = w.remote ? w.box_reply_dev : b_.irecvbuf + size_t(h.slot) * b_.rl;
+      xb.copy(src, b_.recvbuf + size_t(h.slot) * b_.rl, b_.rl);
     }
+    bool local_posts = false;
+    for (int64_t rank : posts_) {
+      const HipWorker& w = w_[size_t(rank - 1)];
+      uint8_t* slot = b_.isendbuf + size_t(w.slot) * b_.sl;
+      if (w.remote) {
+        xb.reserve(2, 1);
+        xb.copy(b_.sendbuf, slot, b_.sl);
+        xb.copy(b_.sendbuf, w.box_msg_dev, b_.sl);
+        xb.door(w.box_door_dev, w.seq);
+      } else {
+        xb.copy(b_.sendbuf, slot, b_.sl);
+        local_posts = true;
+      }
+    }
+    xb.launch();
     harv_.clear();
-    if (posts_.empty()) return;
-    HIPCHECK(hipEventRecord(xfer_ev_, coord_));
-    launch_posts();
+    if (local_posts) {
+      HIPCHECK(hipEventRecord(xfer_ev_, coord_));
+      std::vector<int64_t> here;
+      for (int64_t rank : posts_)
+        if (!w_[size_t(rank - 1)].remote) here.push_back(rank);
+      launch_tasks(here, /*staged=*/false);
+    }
     posts_.clear();
   }
 
@@ -195,42 +328,101 @@ class HipComm final : public Comm {
   }
 
   int64_t tasks_done(int64_t rank) override {
-    return int64_t(__atomic_load_n(&flags_[rank - 1], __ATOMIC_ACQUIRE));
+    return int64_t(__atomic_load_n(w_[size_t(rank - 1)].flag_host, __ATOMIC_ACQUIRE));
   }
 
   void shutdown() override {
-    const auto t0 = Clock::now();
-    for (int64_t r = 1; r <= nworkers_; ++r)
-      for (uint64_t spins = 0; !done(r); ++spins) {
-        if ((spins & 0xFFF) == 0xFFF) watchdog(t0);
-        __builtin_ia32_pause();
+    if (role_ != SERVER) {
+      const auto t0 = Clock::now();
+      for (int64_t r = 1; r <= nworkers_; ++r) {
+        if (!w_[size_t(r - 1)].here && !w_[size_t(r - 1)].remote) continue;
+        for (uint64_t spins = 0; !done(r); ++spins) {
+          if ((spins & 0xFFF) == 0xFFF) watchdog(t0);
+          __builtin_ia32_pause();
+        }
       }
-    for (auto& w : w_) HIPCHECK(hipStreamSynchronize(w.stream));
+      if (region_) __atomic_store_n(&region_->header()->shutdown, 1ull, __ATOMIC_RELEASE);
+    }
+    for (auto& w : w_)
+      if (w.stream) HIPCHECK(hipStreamSynchronize(w.stream));
     for (auto& s : launch_streams_) HIPCHECK(hipStreamSynchronize(s));
     shutdown_ = true;
   }
 
   void on_task_changed(int64_t rank) override {
     HipWorker& w = w_[size_t(rank - 1)];
+    if (!w.here)
+      fail(MPA_ARGUMENT_ERROR, "worker %lld is served by another process; register its task there", (long long)rank);
     if (w.seq != uint64_t(tasks_done(rank)))
       fail(MPA_ERROR, "cannot change the task of worker %lld while it has an outstanding request", (long long)rank);
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
     if (ts.kind == MPA_TASK_LSQ) prepare_lsq(rank, ts);
   }
 
-  unsigned device_error() const { return __atomic_load_n(err_, __ATOMIC_ACQUIRE); }
-
- private:
-  bool done(int64_t rank) const {
-    return __atomic_load_n(&flags_[rank - 1], __ATOMIC_ACQUIRE) >= w_[size_t(rank - 1)].seq;
+  // ---- worker process: watch the doorbells of the workers served here ----
+  void serve() {
+    if (role_ != SERVER) fail(MPA_ERROR, "mpa_comm_serve is for worker processes (rank != 0)");
+    ShmHeader* h = region_->header();
+    const uint64_t gen0 = __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE);
+    const auto t0 = Clock::now();
+    std::vector<int64_t> fresh;
+    for (uint64_t spins = 0;; ++spins) {
+      if (__atomic_load_n(&h->shutdown, __ATOMIC_ACQUIRE) || __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE) != gen0) break;
+      fresh.clear();
+      for (int64_t r = 1; r <= nworkers_; ++r) {
+        HipWorker& w = w_[size_t(r - 1)];
+        if (!w.here) continue;
+        const unsigned long long db = __atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE);
+        if (db == w.seq) continue;
+        if (db != w.seq + 1) fail(MPA_ERROR, "mailbox protocol: worker %lld doorbell %llu after %llu", (long long)r, db, w.seq);
+        if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) != w.seq)
+          fail(MPA_ERROR, "mailbox protocol: worker %lld posted while busy", (long long)r);
+        w.seq = db;
+        w.sl = size_t(w.box->msg_bytes);
+        w.rl = size_t(w.box->reply_bytes);
+        check_task(r, tasks_[size_t(r - 1)], w.sl, w.rl);
+        w.x = w.xslot;
+        w.out = w.box_reply_dev;
+        fresh.push_back(r);
+      }
+      if (!fresh.empty()) {
+        if (timing_) reap_timing(false);
+        launch_tasks(fresh, /*staged=*/true);
+      } else {
+        if ((spins & 0xFFF) == 0xFFF) watchdog(t0, /*timeout=*/false);
+        __builtin_ia32_pause();
+      }
+    }
   }
 
-  void watchdog(Clock::time_point t0) {
+  void pause_servers() {
+    if (role_ != COORD) fail(MPA_ERROR, "only rank 0 of a multi-process communicator pauses its servers");
+    __atomic_fetch_add(&region_->header()->gen, 1ull, __ATOMIC_RELEASE);
+  }
+
+ private:
+  struct Harvest {
+    int64_t slot, rank;
+  };
+
+  bool done(int64_t rank) const {
+    const HipWorker& w = w_[size_t(rank - 1)];
+    return __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) >= w.seq;
+  }
+
+  unsigned device_error() const {
+    unsigned e = __atomic_load_n(err_, __ATOMIC_ACQUIRE);
+    if (region_) e |= __atomic_load_n(&region_->header()->err, __ATOMIC_ACQUIRE);
+    return e;
+  }
+
+  void watchdog(Clock::time_point t0, bool timeout = true) {
     const unsigned e = device_error();
-    if (e) fail(MPA_DEVICE_ERROR, "device-side error word 0x%x (in-kernel wait timed out)", e);
-    for (auto& w : w_) check_stream(w.stream);
+    if (e) fail(MPA_DEVICE_ERROR, "device-side error word 0x%x (an in-kernel wait timed out)", e);
+    for (auto& w : w_)
+      if (w.stream) check_stream(w.stream);
     for (auto& s : launch_streams_) check_stream(s);
-    if (timeout_s_ > 0 && std::chrono::duration<double>(Clock::now() - t0).count() > timeout_s_)
+    if (timeout && timeout_s_ > 0 && std::chrono::duration<double>(Clock::now() - t0).count() > timeout_s_)
       fail(MPA_DEVICE_ERROR, "waited more than %.0f s for a worker (MPA_WAIT_TIMEOUT_S)", timeout_s_);
   }
 
@@ -250,8 +442,8 @@ class HipComm final : public Comm {
         if (rl < size_t(ts.cols) * es)
           fail(MPA_DIMENSION_MISMATCH, "worker %lld (least squares, %lld columns) replies %zu bytes, recv chunk is %zu",
                (long long)rank, (long long)ts.cols, size_t(ts.cols) * es, rl);
-        if ((reinterpret_cast<uintptr_t>(b_.isendbuf) | reinterpret_cast<uintptr_t>(b_.irecvbuf)) % es ||
-            sl % es || rl % es)
+        if (role_ != SERVER &&
+            ((reinterpret_cast<uintptr_t>(b_.isendbuf) | reinterpret_cast<uintptr_t>(b_.irecvbuf)) % es || sl % es || rl % es))
           fail(MPA_ARGUMENT_ERROR, "least-squares buffers must be %zu-byte aligned", es);
         return;
       }
@@ -270,52 +462,65 @@ class HipComm final : public Comm {
       fail(MPA_ARGUMENT_ERROR, "least-squares worker: lda (%lld) must be >= cols and a multiple of %d", (long long)ts.lda, E);
     if (reinterpret_cast<uintptr_t>(ts.A) % 16 || reinterpret_cast<uintptr_t>(ts.b) % size_t(es))
       fail(MPA_ARGUMENT_ERROR, "least-squares worker: A must be 16-byte aligned and b element aligned");
-    const int rpw = lsq_rows_per_wave_iter(ts.dtype, int(ts.cols));
-    const int R = lsq_reducers(ts.dtype, int(ts.cols));
-    int64_t want = (ts.rows + 4 * rpw - 1) / (4 * rpw);
-    const int gmax = g_lsq_grid > 0 ? g_lsq_grid : grid_max_;
-    int grid = int(want < gmax ? want : gmax);
-    if (grid < R) grid = R;
-    const size_t bytes = size_t(grid) * size_t(cp) * size_t(es);
-    if (bytes > w.slab_bytes) {
-      if (w.slab) HIPCHECK(hipFree(w.slab));
+    if (role_ == SERVER && size_t(ts.cols) * size_t(es) > region_->max_msg())
+      fail(MPA_DIMENSION_MISMATCH, "least-squares worker: %zu-byte messages exceed the mailbox", size_t(ts.cols) * es);
+    const int cap = kSlabGridCap;
+    const size_t bytes = size_t(cap) * size_t(cp) * size_t(es);
+    if (!w.slab) {
       HIPCHECK(hipMalloc(&w.slab, bytes));
-      w.slab_bytes = bytes;
+      w.slab_grid = cap;
     }
-    w.grid = grid;
   }
 
-  // Posts of one flush: least-squares tasks without an injected delay run as ONE batched
-  // launch (per kernel variant, <= kMaxLsqTasks each) on an idle launch stream; a task
-  // with a delay runs on its worker's own stream behind a delay kernel, so a straggler
-  // never holds back another worker; reference-test tasks (kmap/echo) run per worker.
-  void launch_posts() {
+  // workgroups per task in a least-squares launch of `ntasks` tasks
+  int lsq_grid(const TaskSpec& ts, const HipWorker& w, int ntasks) const {
+    const int total = g_lsq_grid > 0 ? g_lsq_grid : kDefaultLaunchGrid;
+    const int rpw = lsq_rows_per_wave_iter(ts.dtype, int(ts.cols));
+    const int R = lsq_reducers(ts.dtype, int(ts.cols));
+    const int64_t want = (ts.rows + 4 * rpw - 1) / (4 * rpw);
+    int g = total / (ntasks > 0 ? ntasks : 1);
+    if (g > want) g = int(want);
+    if (g > w.slab_grid) g = w.slab_grid;
+    if (g < R) g = R;
+    return g;
+  }
+
+  // Tasks of one flush (coordinator) or one doorbell scan (server).  Least-squares tasks
+  // without an injected delay run as ONE batched launch (per kernel variant, <=
+  // kMaxLsqTasks each) on an idle launch stream; a task with a delay runs on its worker's
+  // own stream behind a delay kernel, so a straggler never holds back another worker;
+  // reference-test tasks (kmap/echo) run per worker.  `staged`: the message sits in a
+  // mailbox and is first copied into the worker's device slot on the launch's stream.
+  void launch_tasks(const std::vector<int64_t>& ranks, bool staged) {
     std::vector<int64_t> batch;
     int batch_dtype = -1, batch_cp = 0;
-    auto emit = [&](hipStream_t s) {
+    hipStream_t bs = nullptr;
+    auto emit = [&]() {
       if (batch.empty()) return;
-      launch_lsq_batch(batch, batch_dtype, s);
+      bs = pick_launch_stream();
+      if (staged) stage_in(batch, bs);
+      else HIPCHECK(hipStreamWaitEvent(bs, xfer_ev_, 0));
+      launch_lsq_batch(batch, batch_dtype, bs);
       batch.clear();
     };
-    for (int64_t rank : posts_) {
+    for (int64_t rank : ranks) {
       HipWorker& w = w_[size_t(rank - 1)];
       const TaskSpec& ts = tasks_[size_t(rank - 1)];
       int64_t delay = 0;
       if (!ts.delays_ns.empty()) delay = ts.delays_ns[size_t((int64_t(w.seq) - 1) % int64_t(ts.delays_ns.size()))];
       if (ts.kind == MPA_TASK_LSQ && delay == 0) {
         const int cp = lsq_cols_pad(ts.dtype, int(ts.cols));
-        if (!batch.empty() && (ts.dtype != batch_dtype || cp != batch_cp || batch.size() == size_t(kMaxLsqTasks)))
-          emit(pick_launch_stream());
+        if (!batch.empty() && (ts.dtype != batch_dtype || cp != batch_cp || batch.size() == size_t(kMaxLsqTasks))) emit();
         batch_dtype = ts.dtype;
         batch_cp = cp;
         batch.push_back(rank);
         continue;
       }
-      HIPCHECK(hipStreamWaitEvent(w.stream, xfer_ev_, 0));
+      if (staged) stage_in({rank}, w.stream);
+      else HIPCHECK(hipStreamWaitEvent(w.stream, xfer_ev_, 0));
       if (delay > 0) HIPCHECK(launch_delay((unsigned long long)(double(delay) * 1e-9 * rt_hz_), w.stream));
       if (ts.kind == MPA_TASK_LSQ) {
-        std::vector<int64_t> one{rank};
-        launch_lsq_batch(one, ts.dtype, w.stream, /*waited=*/true);
+        launch_lsq_batch({rank}, ts.dtype, w.stream);
       } else {
         KmapArgs a{};
         a.kind = ts.kind;
@@ -324,11 +529,20 @@ class HipComm final : public Comm {
         a.sl = w.sl;
         a.out = w.out;
         a.rl = w.rl;
-        a.pub = Publish{&flags_[rank - 1], err_, w.seq, spin_ticks()};
+        a.pub = Publish{w.flag_dev, err_dev_, w.seq, spin_ticks()};
         HIPCHECK(launch_kmap(a, w.stream));
       }
     }
-    emit(pick_launch_stream());
+    emit();
+  }
+
+  void stage_in(const std::vector<int64_t>& ranks, hipStream_t s) {
+    ExchangeBuilder xb(ticket_, &ticket_count_, s);
+    for (int64_t rank : ranks) {
+      const HipWorker& w = w_[size_t(rank - 1)];
+      xb.copy(w.box_msg_dev, w.xslot, w.sl);
+    }
+    xb.launch();
   }
 
   unsigned long long spin_ticks() const { return (unsigned long long)(timeout_s_ * rt_hz_); }
@@ -349,10 +563,10 @@ class HipComm final : public Comm {
     return s;
   }
 
-  void launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hipStream_t s, bool waited = false) {
+  void launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hipStream_t s) {
     LsqBatch b{};
     b.ntasks = int(ranks.size());
-    b.err = err_;
+    b.err = err_dev_;
     b.spin_ticks = spin_ticks();
     int blocks = 0;
     double bytes = 0;
@@ -367,19 +581,18 @@ class HipComm final : public Comm {
       t.out = w.out;
       t.slab = w.slab;
       t.ctr = ctr_ + 2 * (rank - 1);
-      t.flag = &flags_[rank - 1];
+      t.flag = w.flag_dev;
       t.seq = w.seq;
       t.rows = ts.rows;
       t.lda = ts.lda;
       t.cols = int(ts.cols);
-      t.grid = w.grid;
+      t.grid = lsq_grid(ts, w, b.ntasks);
       b.block0[k] = blocks;
-      blocks += w.grid;
+      blocks += t.grid;
       const double es = dtype == MPA_F64 ? 8.0 : 4.0;
       bytes += es * (double(ts.rows) * double(ts.cols) + double(ts.rows) + 2.0 * double(ts.cols));
     }
     b.block0[b.ntasks] = blocks;
-    if (!waited) HIPCHECK(hipStreamWaitEvent(s, xfer_ev_, 0));
     TimedLaunch tl{};
     if (timing_) {
       tl.start = take_event();
@@ -432,8 +645,12 @@ class HipComm final : public Comm {
     size_t keep = 0;
     for (size_t k = 0; k < timed_.size(); ++k) {
       TimedLaunch& tl = timed_[k];
-      if (block) HIPCHECK(hipEventSynchronize(tl.stop));
-      else if (hipEventQuery(tl.stop) != hipSuccess) { timed_[keep++] = tl; continue; }
+      if (block) {
+        HIPCHECK(hipEventSynchronize(tl.stop));
+      } else if (hipEventQuery(tl.stop) != hipSuccess) {
+        timed_[keep++] = tl;
+        continue;
+      }
       float ms = 0;
       HIPCHECK(hipEventElapsedTime(&ms, tl.start, tl.stop));
       t_ms_ += ms;
@@ -445,6 +662,24 @@ class HipComm final : public Comm {
     timed_.resize(keep);
   }
 
+  Role role_ = SOLO;
+  std::vector<HipWorker> w_;
+  ShmRegion* region_ = nullptr;
+  int my_rank_ = 0;
+  int dev_ = 0;
+  hipStream_t coord_ = nullptr;
+  unsigned long long* flags_ = nullptr;
+  unsigned* err_ = nullptr;
+  unsigned* err_dev_ = nullptr;
+  uint32_t* ctr_ = nullptr;
+  uint32_t* ticket_ = nullptr;
+  uint32_t ticket_count_ = 0;
+  hipEvent_t xfer_ev_ = nullptr;
+  double rt_hz_ = 100e6;
+  double timeout_s_ = 600.0;
+  std::vector<int64_t> posts_;
+  std::vector<Harvest> harv_;
+  CallBufs b_;
   bool timing_ = false;
   std::vector<TimedLaunch> timed_;
   std::vector<hipEvent_t> event_pool_;
@@ -453,26 +688,36 @@ class HipComm final : public Comm {
   std::vector<hipStream_t> launch_streams_;
   size_t next_launch_ = 0;
 
-  int dev_ = 0;
-  hipStream_t coord_ = nullptr;
-  std::vector<HipWorker> w_;
-  unsigned long long* flags_ = nullptr;
-  unsigned* err_ = nullptr;
-  uint32_t* ctr_ = nullptr;
-  hipEvent_t xfer_ev_ = nullptr;
-  double rt_hz_ = 100e6;
-  int grid_max_ = 512;
-  double timeout_s_ = 600.0;
-  std::vector<int64_t> posts_, harv_;
-  CallBufs b_;
+ public:
+  void init_ticket() { ticket_ = ctr_ + 2 * nworkers_; }
 };
 
 }  // namespace
 
-Comm* make_hip_comm(int64_t nworkers, const int* devices) { return new HipComm(nworkers, devices); }
+Comm* make_hip_comm(int64_t nworkers, const int* devices) {
+  HipComm* c = new HipComm(nworkers, devices, nullptr, 0, nullptr);
+  c->init_ticket();
+  return c;
+}
+
+Comm* make_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg) {
+  if (!placement) fail(MPA_ARGUMENT_ERROR, "placement is NULL");
+  if (!shm_name || !*shm_name) fail(MPA_ARGUMENT_ERROR, "shared memory name is empty");
+  for (int64_t i = 0; i < nworkers; ++i)
+    if (placement[i] < 0) fail(MPA_ARGUMENT_ERROR, "placement of worker %lld is negative", (long long)(i + 1));
+  std::unique_ptr<ShmRegion> r(my_rank == 0 ? ShmRegion::create(shm_name, nworkers, max_msg)
+                                            : ShmRegion::attach(shm_name));
+  HipComm* c = new HipComm(nworkers, nullptr, placement, my_rank, r.get());
+  r.release();
+  c->init_ticket();
+  return c;
+}
+
 void hip_set_stream(Comm* c, void* s) { static_cast<HipComm*>(c)->set_stream(static_cast<hipStream_t>(s)); }
 void* hip_get_stream(Comm* c) { return static_cast<HipComm*>(c)->stream(); }
 void hip_set_timing(Comm* c, bool on) { static_cast<HipComm*>(c)->set_timing(on); }
 void hip_timing(Comm* c, double out[3]) { static_cast<HipComm*>(c)->timing(out); }
+void hip_serve(Comm* c) { static_cast<HipComm*>(c)->serve(); }
+void hip_pause_servers(Comm* c) { static_cast<HipComm*>(c)->pause_servers(); }
 
 }  // namespace mpa

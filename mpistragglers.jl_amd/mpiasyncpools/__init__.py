@@ -3,11 +3,11 @@
 completion words.  See DESIGN.md at the repository root.
 """
 from ._capi import lib  # noqa: F401  (fails loudly if the HIP library is not built)
-from .comm import DeviceComm, SimComm, generate  # noqa: F401
+from .comm import DeviceComm, DistComm, SimComm, generate  # noqa: F401
 from .pool import (ArgumentError, DeviceError, DimensionMismatch, ErrorException,  # noqa: F401
                    MPIAsyncPool, asyncmap, asyncmap_, waitall, waitall_)
 
 lib()
 
-__all__ = ["MPIAsyncPool", "asyncmap_", "waitall_", "asyncmap", "waitall", "DeviceComm", "SimComm",
+__all__ = ["MPIAsyncPool", "asyncmap_", "waitall_", "asyncmap", "waitall", "DeviceComm", "DistComm", "SimComm",
            "generate", "ArgumentError", "DimensionMismatch", "ErrorException", "DeviceError"]

@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(PKG_ROOT, "_build", "libmpiasyncpools.so")
 
 MPA_OK, MPA_ARGUMENT_ERROR, MPA_DIMENSION_MISMATCH, MPA_ERROR, MPA_DEVICE_ERROR, MPA_CALLBACK_ERROR = range(6)
 MPA_F32, MPA_F64, MPA_BF16 = 0, 1, 2
-MPA_TRANSPORT_HIP, MPA_TRANSPORT_SIM = 0, 1
+MPA_TRANSPORT_HIP, MPA_TRANSPORT_SIM, MPA_TRANSPORT_HOST = 0, 1, 2
 MPA_NWAIT_INT, MPA_NWAIT_FN, MPA_NWAIT_OTHER = 0, 1, 2
 (MPA_TASK_NONE, MPA_TASK_ECHO, MPA_TASK_KMAP1, MPA_TASK_KMAP2, MPA_TASK_LSQ,
  MPA_TASK_LSQ_BATCH) = range(6)
@@ -52,6 +52,9 @@ SIGNATURES = [
     ("mpa_comm_set_delays", C.c_int, [_vp, C.c_int64, _vp, C.c_int64]),
     ("mpa_comm_tasks_done", C.c_int64, [_vp, C.c_int64]),
     ("mpa_comm_shutdown", C.c_int, [_vp]),
+    ("mpa_comm_create_dist", C.c_int, [C.c_int, C.c_int64, _vp, C.c_int, C.c_char_p, _sz, C.POINTER(_vp)]),
+    ("mpa_comm_serve", C.c_int, [_vp]),
+    ("mpa_comm_pause_servers", C.c_int, [_vp]),
     ("mpa_comm_set_timing", C.c_int, [_vp, C.c_int]),
     ("mpa_comm_timing", C.c_int, [_vp, C.POINTER(C.c_double)]),
     ("mpa_comm_sim_set_compute", C.c_int, [_vp, C.c_int64]),

@@ -33,15 +33,24 @@ def dtype_code(a):
 class _Comm:
     transport = None
 
-    def __init__(self, nworkers, devices=None):
+    def __init__(self, nworkers, devices=None, _handle=None):
         h = C.c_void_p()
-        dev = None
-        if devices is not None:
-            dev = (C.c_int * nworkers)(*devices)
-        check(lib().mpa_comm_create(self.transport, int(nworkers), dev, C.byref(h)))
+        if _handle is not None:
+            h = _handle
+        else:
+            dev = None
+            if devices is not None:
+                dev = (C.c_int * nworkers)(*devices)
+            check(lib().mpa_comm_create(self.transport, int(nworkers), dev, C.byref(h)))
         self._h = h
         self.nworkers = int(nworkers)
         self._keep = {}
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def size(self):
         """MPI.Comm_size: workers + the coordinator."""
@@ -134,6 +143,44 @@ class DeviceComm(_Comm):
         check(lib().mpa_lsq_update(self._h, dtype_code(x), C.c_void_p(x.data_ptr()),
                                    C.c_void_p(recvbuf.data_ptr()), int(nchunks), int(x.numel()),
                                    w.ctypes.data, float(eta)))
+
+
+class DistComm(DeviceComm):
+    """One process per GPU.
+
+    Every rank constructs it with the same `placement` (placement[w-1] = the process rank
+    serving worker w) and `shm_name`; rank 0 must construct it first (it creates the
+    shared-memory mailboxes).  Rank 0 is the coordinator and calls asyncmap_/waitall_;
+    every other rank registers the tasks of its workers and calls serve(), which returns
+    when rank 0 calls pause_servers() or shutdown().  transport="host" runs the same
+    protocol with host-executed test workers (echo/kmap1/kmap2) and no GPU."""
+
+    def __init__(self, nworkers, placement, rank, shm_name, max_msg_bytes, transport="hip"):
+        code = {"hip": _capi.MPA_TRANSPORT_HIP, "host": _capi.MPA_TRANSPORT_HOST}[transport]
+        if code == _capi.MPA_TRANSPORT_HIP:
+            import torch
+            if not torch.cuda.is_available():
+                raise RuntimeError("DistComm(transport='hip') needs a GPU (HIP); no device is visible")
+            torch.cuda.init()
+        pl = (C.c_int * nworkers)(*[int(p) for p in placement])
+        h = C.c_void_p()
+        check(lib().mpa_comm_create_dist(code, int(nworkers), pl, int(rank), shm_name.encode(), int(max_msg_bytes),
+                                         C.byref(h)))
+        self.transport = code
+        self.rank = int(rank)
+        self.placement = list(placement)
+        _Comm.__init__(self, nworkers, _handle=h)
+
+    def _before_call(self, sendbuf):
+        if self.transport == _capi.MPA_TRANSPORT_HIP:
+            DeviceComm._before_call(self, sendbuf)
+
+    def serve(self):
+        """Worker processes: serve this rank's workers until rank 0 pauses or shuts down."""
+        check(lib().mpa_comm_serve(self._h))
+
+    def pause_servers(self):
+        check(lib().mpa_comm_pause_servers(self._h))
 
 
 class SimComm(_Comm):

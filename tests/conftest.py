@@ -3,11 +3,6 @@ import sys
 
 import pytest
 
-# One HSA queue per stream: HIP serialises every kernel of streams that share a hardware
-# queue, so a straggler's delay kernel would otherwise hold back unrelated workers.  Must be
-# set before the HIP runtime initialises (DESIGN.md §Streams and queues).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "mpistragglers.jl_amd"), os.path.join(ROOT, "oracle")):
     if p not in sys.path:

@@ -1,0 +1,175 @@
+"""Per-rank bodies of the multi-process tests (spawned by tests/test_dist_cpu.py and
+tests/test_gpu_dist.py).  Rank 0 is the coordinator; the other ranks serve the workers
+placed on them.  Mirrors test/kmap2.jl with the workers spread over processes (as the
+reference's MPI ranks are) instead of living in the coordinator's process."""
+import os
+import sys
+import traceback
+import uuid
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "mpistragglers.jl_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def kmap2_dist(rank, world, port, transport, placement, result_q):
+    """kmap2.jl semantics with workers on ranks `placement`; rank 0 reports failures."""
+    import numpy as np
+    try:
+        dist = _init(rank, world, port)
+        if transport == "hip":
+            import torch
+            torch.cuda.set_device(0)
+        import mpiasyncpools as M
+        n = len(placement)
+        name = [f"/mpa_t{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+        if rank == 0:
+            comm = M.DistComm(n, placement, 0, name[0], 256, transport=transport)
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            comm = M.DistComm(n, placement, rank, name[0], 256, transport=transport)
+        rng = np.random.default_rng(7)
+        delays = (np.maximum(rng.random((n, 64)) / 10, 0.005) * 2e7).astype(np.int64)  # 0.1-2 ms
+        for w in range(1, n + 1):
+            if placement[w - 1] == rank:
+                comm.set_task(w, "kmap2")
+                comm.set_delays(w, delays[w - 1])
+        dist.barrier()
+        if rank != 0:
+            comm.serve()          # session 1
+            dist.barrier()
+            comm.serve()          # session 2, until shutdown
+            dist.barrier()
+            comm.close()
+            dist.destroy_process_group()
+            return
+        if transport == "hip":
+            import torch
+
+            def buf(k):
+                return torch.zeros(k, dtype=torch.float64, device="cuda")
+            host = lambda t: t.cpu().numpy()  # noqa: E731
+        else:
+            def buf(k):
+                return np.zeros(k)
+            host = lambda t: t  # noqa: E731
+        pool = M.MPIAsyncPool(n)
+        sendbuf, isendbuf = buf(1), buf(n)
+        recvbuf, irecvbuf = buf(3 * n), buf(3 * n)
+        errors = []
+        for epoch in range(1, 41):
+            sendbuf[0] = epoch
+            rep = M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=2)
+            rb = host(recvbuf).reshape(n, 3)
+            fresh = 0
+            for i in range(n):
+                if rep[i] == 0:
+                    continue
+                fresh += rep[i] == epoch
+                if rb[i, 2] != rep[i] or rb[i, 0] != i + 1:
+                    errors.append(("integrity", epoch, i, rb[i].tolist(), int(rep[i])))
+            if fresh < 2:
+                errors.append(("fresh", epoch, rep.tolist()))
+        comm.pause_servers()
+        dist.barrier()
+        for _ in range(10):
+            M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=1)
+            M.waitall_(pool, recvbuf, irecvbuf)
+            if pool.active.any():
+                errors.append(("waitall", pool.active.tolist()))
+        f = lambda e, r: bool(r[0] == e)  # noqa: E731
+        for _ in range(10):
+            rep = M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=f)
+            if rep[0] != pool.epoch:
+                errors.append(("predicate", rep.tolist(), pool.epoch))
+        M.waitall_(pool, recvbuf, irecvbuf)
+        rb = host(recvbuf).reshape(n, 3)
+        for i in range(n):
+            if rb[i, 1] != comm.tasks_done(i + 1):
+                errors.append(("t", i, rb[i].tolist(), comm.tasks_done(i + 1)))
+        comm.shutdown()
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        result_q.put(("ok", errors))
+    except Exception:
+        result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
+        raise
+
+
+def lsq_dist(rank, world, port, placement, result_q):
+    """Least-squares workers on several processes: each rank generates the shards of its
+    workers on its GPU (Philox layout); rank 0 checks every chunk against the fp64 oracle
+    gradient of the iterate sent at epoch repochs[i]."""
+    import numpy as np
+    try:
+        dist = _init(rank, world, port)
+        import torch
+        torch.cuda.set_device(0)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import mpiasyncpools as M
+        n, rows, cols, seed = len(placement), 4096, 1024, 21
+        name = [f"/mpa_l{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+        if rank == 0:
+            comm = M.DistComm(n, placement, 0, name[0], cols * 4, transport="hip")
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            comm = M.DistComm(n, placement, rank, name[0], cols * 4, transport="hip")
+        keep = []
+        for w in range(1, n + 1):
+            if placement[w - 1] == rank:
+                A = torch.empty(rows, cols, device="cuda")
+                b = torch.empty(rows, device="cuda")
+                M.generate(A, seed, 0, (w - 1) * rows * cols, float(np.float32(1 / np.sqrt(cols))))
+                M.generate(b, seed, 1, (w - 1) * rows, 1.0)
+                keep.append((A, b))
+                comm.set_task_lsq(w, A, b)
+                comm.set_delays(w, [0, 2_000_000, 0, 0, 5_000_000][w % 5:] + [0])
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank != 0:
+            comm.serve()
+            dist.barrier()
+            comm.close()
+            dist.destroy_process_group()
+            return
+        import lsq
+        A_all = lsq.gen_matrix(seed, 0, n * rows, cols, "f32")
+        b_all = lsq.gen_vector(seed, 0, n * rows, "f32")
+        pool = M.MPIAsyncPool(n)
+        x = torch.zeros(cols, device="cuda")
+        isend = torch.zeros(n * cols, device="cuda")
+        recv = torch.zeros(n * cols, device="cuda")
+        irecv = torch.zeros_like(recv)
+        sent, errors = {}, []
+        for epoch in range(1, 11):
+            sent[epoch] = x.cpu().numpy().copy()
+            rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=3)
+            ch = recv.cpu().numpy().reshape(n, cols)
+            for i in range(n):
+                if rep[i] == 0:
+                    continue
+                g = lsq.shard_gradient(A_all[i * rows:(i + 1) * rows], b_all[i * rows:(i + 1) * rows], sent[int(rep[i])])
+                e = lsq.rel_err(ch[i], g)
+                if not e <= 1e-5:
+                    errors.append(("grad", epoch, i, int(rep[i]), e))
+            w = (rep == epoch).astype(np.float64) * (n / max(1, int((rep == epoch).sum())))
+            comm.lsq_update(x, recv, n, w, 0.05)
+        M.waitall_(pool, recv, irecv)
+        comm.shutdown()
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        result_q.put(("ok", errors))
+    except Exception:
+        result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
+        raise

@@ -1,0 +1,44 @@
+"""The multi-process HIP transport on a GPU box: rank 0 coordinates, rank 1 (a second
+process on the same GPU) serves workers through the shared-memory mailboxes; kmap2.jl
+properties across processes and a least-squares epoch checked against the fp64 oracle."""
+import multiprocessing as mp
+import random
+
+import pytest
+
+import dist_worker
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(target, world, *args, timeout=180):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        status, payload = q.get(timeout=timeout)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert status == "ok", payload
+    assert payload == [], payload
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_kmap2_two_processes_hip(built):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.kmap2_dist, 2, "hip", [0, 1, 1, 1])
+
+
+def test_lsq_two_processes_hip(built):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.lsq_dist, 2, [0, 1, 1, 1])

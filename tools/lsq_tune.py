@@ -14,7 +14,6 @@ import os
 import sys
 import time
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpistragglers.jl_amd"))
 
@@ -29,8 +28,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--epochs", type=int, default=20)
-    ap.add_argument("--grids", default="64,128,256,512")
-    ap.add_argument("--variants", default="")
+    ap.add_argument("--grids", default="32,48,64,96,128")
+    ap.add_argument("--variants", default="2,4,5,6")
     a = ap.parse_args()
     n, rows, cols = 8, 1 << 20, 1024
     per = rows // n
