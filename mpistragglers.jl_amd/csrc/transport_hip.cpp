@@ -28,9 +28,11 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 
 #include "comm.hpp"
 #include "kernels.hpp"
@@ -53,7 +55,23 @@ constexpr int kDefaultLaunchGrid = 512;  // 2 workgroups per CU: profiles/r01_tu
 constexpr int kSlabGridCap = 1024;       // most workgroups a single task may be given
 constexpr int kLaunchStreams = 2;
 
+// Process-wide pool of CU-masked streams: communicators come and go (tests create many),
+// but the HSA queues behind their streams are a bounded hardware resource, so a destroyed
+// comm returns its streams here and the next comm reuses them instead of growing the
+// process's queue count (more queues than the hardware maps at once are time-sliced).
+std::mutex g_stream_mu;
+std::vector<std::pair<int, hipStream_t>> g_free_streams;
+
 hipStream_t make_queue_stream(int device) {
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    for (size_t k = 0; k < g_free_streams.size(); ++k)
+      if (g_free_streams[k].first == device) {
+        hipStream_t s = g_free_streams[k].second;
+        g_free_streams.erase(g_free_streams.begin() + std::ptrdiff_t(k));
+        return s;
+      }
+  }
   hipDeviceProp_t p;
   HIPCHECK(hipGetDeviceProperties(&p, device));
   const int cus = p.multiProcessorCount;
@@ -62,6 +80,12 @@ hipStream_t make_queue_stream(int device) {
   hipStream_t s = nullptr;
   HIPCHECK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
   return s;
+}
+
+void release_queue_stream(int device, hipStream_t s) {
+  (void)hipStreamSynchronize(s);
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  g_free_streams.push_back({device, s});
 }
 
 struct HipWorker {
@@ -199,6 +223,13 @@ class HipComm final : public Comm {
     rt_hz_ = khz > 0 ? double(khz) * 1e3 : 100e6;
     const char* t = std::getenv("MPA_WAIT_TIMEOUT_S");
     timeout_s_ = t ? std::atof(t) : 600.0;
+    const char* dbg = std::getenv("MPA_DEBUG");
+    debug_ = dbg && *dbg == '1';
+    if (debug_ && region_) {
+      std::fprintf(stderr, "[mpa role %d rank %d] shm header %p (device %p)\n", int(role_), my_rank_,
+                   (void*)region_->header(), (void*)region_->dev(region_->header()));
+      describe("shm", region_->dev(region_->header()));
+    }
     HIPCHECK(hipDeviceSynchronize());
   }
 
@@ -207,9 +238,9 @@ class HipComm final : public Comm {
     for (auto& w : w_) {
       if (w.slab) (void)hipFree(w.slab);
       if (w.xslot) (void)hipFree(w.xslot);
-      if (w.stream) (void)hipStreamDestroy(w.stream);
+      if (w.stream) release_queue_stream(dev_, w.stream);
     }
-    for (auto& s : launch_streams_) (void)hipStreamDestroy(s);
+    for (auto& s : launch_streams_) release_queue_stream(dev_, s);
     for (auto& t : timed_) {
       (void)hipEventDestroy(t.start);
       (void)hipEventDestroy(t.stop);
@@ -540,9 +571,33 @@ class HipComm final : public Comm {
     ExchangeBuilder xb(ticket_, &ticket_count_, s);
     for (int64_t rank : ranks) {
       const HipWorker& w = w_[size_t(rank - 1)];
+      if (debug_) {
+        std::fprintf(stderr, "[mpa role %d] stage-in worker %lld: %zu bytes %p -> %p\n", int(role_), (long long)rank, w.sl,
+                     (void*)w.box_msg_dev, (void*)w.xslot);
+        describe("box msg", w.box_msg_dev);
+        describe("xslot", w.xslot);
+      }
       xb.copy(w.box_msg_dev, w.xslot, w.sl);
     }
     xb.launch();
+    if (debug_) {
+      const hipError_t e = hipStreamSynchronize(s);
+      std::fprintf(stderr, "[mpa role %d] stage-in done: %s\n", int(role_), hipGetErrorString(e));
+      std::fflush(stderr);
+    }
+  }
+
+  // MPA_DEBUG=1: pointer attributes of everything handed to a kernel
+  static void describe(const char* what, const void* p) {
+    hipPointerAttribute_t at;
+    const hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+      std::fprintf(stderr, "    %-8s %p: hipPointerGetAttributes failed: %s\n", what, p, hipGetErrorString(e));
+      (void)hipGetLastError();
+      return;
+    }
+    std::fprintf(stderr, "    %-8s %p: type %d device %d devptr %p hostptr %p\n", what, p, int(at.type), at.device,
+                 at.devicePointer, at.hostPointer);
   }
 
   unsigned long long spin_ticks() const { return (unsigned long long)(timeout_s_ * rt_hz_); }
@@ -600,7 +655,25 @@ class HipComm final : public Comm {
       tl.bytes = bytes;
       HIPCHECK(hipEventRecord(tl.start, s));
     }
+    if (debug_) {
+      for (int k = 0; k < b.ntasks; ++k) {
+        const LsqTask& t = b.t[k];
+        std::fprintf(stderr, "[mpa role %d] lsq task %lld seq %llu grid %d A %p b %p x %p out %p slab %p ctr %p flag %p\n",
+                     int(role_), (long long)ranks[size_t(k)], t.seq, t.grid, t.A, t.b, t.x, t.out, t.slab, (void*)t.ctr,
+                     (void*)t.flag);
+        describe("A", t.A);
+        describe("x", t.x);
+        describe("out", t.out);
+        describe("flag", t.flag);
+      }
+      std::fflush(stderr);
+    }
     HIPCHECK(launch_lsq(dtype, int(tasks_[size_t(ranks[0] - 1)].cols), b, s));
+    if (debug_) {
+      const hipError_t e = hipStreamSynchronize(s);
+      std::fprintf(stderr, "[mpa role %d] lsq launch done: %s\n", int(role_), hipGetErrorString(e));
+      std::fflush(stderr);
+    }
     if (timing_) {
       HIPCHECK(hipEventRecord(tl.stop, s));
       timed_.push_back(tl);
@@ -681,6 +754,7 @@ class HipComm final : public Comm {
   std::vector<Harvest> harv_;
   CallBufs b_;
   bool timing_ = false;
+  bool debug_ = false;
   std::vector<TimedLaunch> timed_;
   std::vector<hipEvent_t> event_pool_;
   int64_t t_launches_ = 0;
