@@ -193,6 +193,18 @@ int mpa_aggregate(mpa_comm* comm, int dtype, const void* recvbuf, int64_t nchunk
 int mpa_lsq_update(mpa_comm* comm, int dtype, void* x, const void* recvbuf, int64_t nchunks,
                    int64_t cols, const double* weights, double eta);
 
+/* The coordinator loop of the least-squares example in native code (the structure of
+ * examples/iterative_example.jl:37-47 with the BASELINE workload): `epochs` iterations of
+ *     repochs = asyncmap!(pool, x, recvbuf, isendbuf, irecvbuf, comm; nwait)
+ *     w_i = 1 (repochs[i] == epoch), stale_weight (older result), 0 (none yet)
+ *     x  -= eta * n / sum(w) * sum_i w_i * g_i                      (mpa_lsq_update)
+ * Each iteration makes exactly the calls a caller's loop makes (mpa_asyncmap, then
+ * mpa_lsq_update), without an interpreter between them.  x holds cols elements; recvbuf,
+ * isendbuf and irecvbuf hold n * cols. */
+int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols, void* recvbuf,
+                    void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
+                    void* nwait_ctx, double eta, double stale_weight, int64_t epochs);
+
 /* ---- synthetic data (device): Philox4x32-10 layout of DESIGN.md §Data ------------- */
 /* out[k] = unit(philox(seed, stream, e0 + k)) * scale, k < count, dtype F32/F64/BF16 */
 int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count,

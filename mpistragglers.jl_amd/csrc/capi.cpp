@@ -330,6 +330,39 @@ int mpa_lsq_update(mpa_comm* comm, int dtype, void* x, const void* recvbuf, int6
   return aggregate_impl(comm, dtype, recvbuf, nchunks, cols, weights, x, 1, eta);
 }
 
+int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols, void* recvbuf, void* isendbuf,
+                    void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn, void* nwait_ctx, double eta,
+                    double stale_weight, int64_t epochs) {
+  int rc = guarded([&] {
+    if (!pool) mpa::fail(MPA_ARGUMENT_ERROR, "pool is NULL");
+    if (dtype != MPA_F32 && dtype != MPA_F64) mpa::fail(MPA_ARGUMENT_ERROR, "lsq_descent: dtype must be F32 or F64");
+    if (cols <= 0 || epochs < 0) mpa::fail(MPA_ARGUMENT_ERROR, "lsq_descent: bad cols / epochs");
+  });
+  if (rc != MPA_OK) return rc;
+  mpa::Pool& p = pool->p;
+  const int64_t n = p.n;
+  const size_t es = dtype == MPA_F64 ? 8 : 4;
+  const size_t sl = size_t(cols) * es, tot = size_t(n) * sl;
+  std::vector<double> w(static_cast<size_t>(n), 0.0);
+  for (int64_t e = 0; e < epochs; ++e) {
+    rc = mpa_asyncmap(pool, x, sl, recvbuf, tot, size_t(n * cols), isendbuf, tot, irecvbuf, tot, comm, nwait_kind,
+                      nwait, nwait_fn, nwait_ctx, "Int64", p.epoch + 1, 0, nullptr);
+    if (rc != MPA_OK) return rc;
+    double sum = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t r = p.repochs[size_t(i)];
+      // repochs[i] == 0: nothing received yet (the convention of test/kmap2.jl:76)
+      w[size_t(i)] = r == p.epoch ? 1.0 : (r > 0 ? stale_weight : 0.0);
+      sum += w[size_t(i)];
+    }
+    const double s = sum > 0 ? double(n) / sum : 0.0;
+    for (auto& v : w) v *= s;
+    rc = mpa_lsq_update(comm, dtype, x, recvbuf, n, cols, w.data(), eta);
+    if (rc != MPA_OK) return rc;
+  }
+  return MPA_OK;
+}
+
 int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count, double scale,
                  void* hip_stream) {
   return guarded([&] {

@@ -1,13 +1,13 @@
 """MI355X-native MPIAsyncPools: the `asyncmap!` hot path of MPIAsyncPools.jl
-(severinson/MPIStragglers.jl) over HIP streams, device task kernels and host-pinned
+(severinson/MPIStragglers.jl) over HIP streams, device task kernels and host-visible
 completion words.  See DESIGN.md at the repository root.
 """
 from ._capi import lib  # noqa: F401  (fails loudly if the HIP library is not built)
 from .comm import DeviceComm, DistComm, SimComm, generate  # noqa: F401
 from .pool import (ArgumentError, DeviceError, DimensionMismatch, ErrorException,  # noqa: F401
-                   MPIAsyncPool, asyncmap, asyncmap_, waitall, waitall_)
+                   MPIAsyncPool, asyncmap, asyncmap_, lsq_descent, waitall, waitall_)
 
 lib()
 
-__all__ = ["MPIAsyncPool", "asyncmap_", "waitall_", "asyncmap", "waitall", "DeviceComm", "DistComm", "SimComm",
-           "generate", "ArgumentError", "DimensionMismatch", "ErrorException", "DeviceError"]
+__all__ = ["MPIAsyncPool", "asyncmap_", "waitall_", "asyncmap", "waitall", "lsq_descent", "DeviceComm", "DistComm",
+           "SimComm", "generate", "ArgumentError", "DimensionMismatch", "ErrorException", "DeviceError"]

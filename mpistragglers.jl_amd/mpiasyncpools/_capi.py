@@ -62,6 +62,8 @@ SIGNATURES = [
     ("mpa_comm_sim_now", C.c_int64, [_vp]),
     ("mpa_aggregate", C.c_int, [_vp, C.c_int, _vp, C.c_int64, C.c_int64, _vp, _vp]),
     ("mpa_lsq_update", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int64, C.c_int64, _vp, C.c_double]),
+    ("mpa_lsq_descent", C.c_int, [_vp, _vp, C.c_int, _vp, C.c_int64, _vp, _vp, _vp, C.c_int, C.c_int64, _vp, _vp,
+                                  C.c_double, C.c_double, C.c_int64]),
     ("mpa_generate", C.c_int, [_vp, C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_int64, C.c_double, _vp]),
 ]
 

@@ -186,5 +186,20 @@ def waitall_(pool, recvbuf, irecvbuf):
     return pool.repochs
 
 
+def lsq_descent(pool, comm, x, recvbuf, isendbuf, irecvbuf, nwait, eta, epochs, stale_weight=0.0):
+    """`epochs` iterations of the least-squares coordinator loop in native code
+    (mpa_lsq_descent): asyncmap_(...; nwait) then x -= eta * n/sum(w) * sum_i w_i g_i with
+    w_i = 1 for fresh chunks, stale_weight for older ones."""
+    from .comm import dtype_code
+    if not isinstance(nwait, (int, np.integer)) or isinstance(nwait, bool):
+        raise ArgumentError("lsq_descent takes an integer nwait")
+    comm._before_call(x)
+    check(lib().mpa_lsq_descent(pool._h, comm._h, dtype_code(x), C.c_void_p(x.data_ptr()), int(x.numel()),
+                                C.c_void_p(recvbuf.data_ptr()), C.c_void_p(isendbuf.data_ptr()),
+                                C.c_void_p(irecvbuf.data_ptr()), _capi.MPA_NWAIT_INT, int(nwait), None, None,
+                                float(eta), float(stale_weight), int(epochs)))
+    return pool.repochs
+
+
 asyncmap = asyncmap_
 waitall = waitall_

@@ -333,3 +333,35 @@ def test_full_size_c2_against_torch_fp64(M, torch_mod):
         del Ai
     # isendbuf holds n copies of x (the reference's isendbufs[i] .= sendbuf, :130)
     assert torch.equal(isend.view(n, cols), x.expand(n, cols))
+
+
+def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod):
+    """mpa_lsq_descent makes the same calls as the Python loop: identical iterates (bitwise,
+    nwait = n so every epoch is fresh and every kernel is deterministic)."""
+    import lsq
+    torch = torch_mod
+    n, rows, cols, seed = 4, 2048, 1024, 17
+    A = _dev(torch, lsq.gen_matrix(seed, 0, n * rows, cols, "f32"))
+    b = _dev(torch, lsq.gen_vector(seed, 0, n * rows, "f32"))
+    xs = []
+    for native in (False, True):
+        comm = M.DeviceComm(n)
+        for r in range(1, n + 1):
+            comm.set_task_lsq(r, A[(r - 1) * rows:r * rows], b[(r - 1) * rows:r * rows])
+        pool = M.MPIAsyncPool(n)
+        x = torch.zeros(cols, device="cuda")
+        isend = torch.zeros(n * cols, device="cuda")
+        recv = torch.zeros(n * cols, device="cuda")
+        irecv = torch.zeros_like(recv)
+        if native:
+            M.lsq_descent(pool, comm, x, recv, isend, irecv, n, 0.01, 6)
+        else:
+            for _ in range(6):
+                rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=n)
+                comm.lsq_update(x, recv, n, (rep == pool.epoch) * 1.0, 0.01)
+        torch.cuda.synchronize()
+        assert pool.epoch == 6
+        xs.append(x.clone())
+        comm.close()
+    assert torch.equal(xs[0].view(torch.int32), xs[1].view(torch.int32))
+    assert float(torch.linalg.norm(xs[0])) > 0
