@@ -4,7 +4,6 @@
 //   exchange_kernel   the reference's byte copies `isendbufs[i] .= sendbuf` (:130,:178) and
 //                     `recvbufs[i] .= irecvbufs[i]` (:108,:167,:216), batched per flush
 //   kmap_task_kernel  the reference's test worker programs (test/kmap1.jl, test/kmap2.jl)
-//   delay_kernel      straggler emulation (the reference's `sleep(rand())`, iterative_example.jl:74)
 //   aggregate_kernel  coordinator consumption of fresh chunks (iterative_example.jl:41-46)
 //   generate_kernel   Philox4x32-10 synthetic data, bit-identical to oracle/philox.h
 //
@@ -86,12 +85,6 @@ __global__ void __launch_bounds__(64) kmap_task_kernel(KmapArgs a) {
   if (threadIdx.x == 0) publish_done(a.pub.flag, a.pub.seq);
 }
 
-__global__ void delay_kernel(unsigned long long ticks) {
-  if (threadIdx.x != 0) return;
-  const unsigned long long t0 = rt_now();
-  while (rt_now() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
-}
-
 // ---------------------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(kThreads) aggregate_kernel(AggregateArgs a) {
@@ -164,11 +157,6 @@ hipError_t launch_exchange(const ExchangeArgs& a, hipStream_t s) {
 
 hipError_t launch_kmap(const KmapArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(kmap_task_kernel, dim3(1), dim3(64), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_delay(unsigned long long ticks, hipStream_t s) {
-  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, ticks);
   return hipGetLastError();
 }
 

@@ -49,6 +49,9 @@ struct LsqTask {
   uint32_t* ctr;    // [2] monotonic arrival counters (device memory)
   unsigned long long* flag;  // host-pinned completion word of the worker
   unsigned long long seq;
+  // ctr[0] / ctr[1] values before this launch.  Launch grids vary with the batch a task
+  // lands in, so the host keeps the running totals (not seq * grid).
+  uint32_t base0, base1;
   int64_t rows, lda;
   int cols, grid;
 };
@@ -83,7 +86,6 @@ struct KmapArgs {
 };
 hipError_t launch_kmap(const KmapArgs& a, hipStream_t s);
 
-hipError_t launch_delay(unsigned long long ticks, hipStream_t s);
 
 constexpr int kMaxAggregate = 256;
 struct AggregateArgs {

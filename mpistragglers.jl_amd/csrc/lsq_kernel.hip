@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   __syncthreads();
 
   const unsigned G = unsigned(a.grid);
-  const unsigned base0 = unsigned((a.seq - 1ull) * G);
+  const unsigned base0 = a.base0;
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     drain_vm();
@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     drain_vm();
-    const unsigned base1 = unsigned((a.seq - 1ull) * unsigned(R));
+    const unsigned base1 = a.base1;
     const unsigned old = __hip_atomic_fetch_add(&a.ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old - base1 == unsigned(R - 1)) publish_done(a.flag, a.seq);
   }

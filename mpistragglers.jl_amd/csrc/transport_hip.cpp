@@ -27,12 +27,18 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
+#include <string>
+#include <thread>
 
 #include "comm.hpp"
 #include "kernels.hpp"
@@ -95,6 +101,7 @@ struct HipWorker {
   unsigned long long seq = 0;  // coordinator: tasks posted; server: tasks served
   void* slab = nullptr;
   int slab_grid = 0;
+  uint32_t ctr0 = 0, ctr1 = 0;  // running totals of this worker's two arrival counters
   // current task
   int64_t slot = -1;
   const uint8_t* x = nullptr;
@@ -234,6 +241,7 @@ class HipComm final : public Comm {
   }
 
   ~HipComm() override {
+    stop_timer();
     (void)hipDeviceSynchronize();
     for (auto& w : w_) {
       if (w.slab) (void)hipFree(w.slab);
@@ -374,6 +382,7 @@ class HipComm final : public Comm {
       }
       if (region_) __atomic_store_n(&region_->header()->shutdown, 1ull, __ATOMIC_RELEASE);
     }
+    drain_deferred();
     for (auto& w : w_)
       if (w.stream) HIPCHECK(hipStreamSynchronize(w.stream));
     for (auto& s : launch_streams_) HIPCHECK(hipStreamSynchronize(s));
@@ -448,6 +457,7 @@ class HipComm final : public Comm {
   }
 
   void watchdog(Clock::time_point t0, bool timeout = true) {
+    check_timer();
     const unsigned e = device_error();
     if (e) fail(MPA_DEVICE_ERROR, "device-side error word 0x%x (an in-kernel wait timed out)", e);
     for (auto& w : w_)
@@ -547,11 +557,17 @@ class HipComm final : public Comm {
         batch.push_back(rank);
         continue;
       }
+      // The message is delivered now (stream-ordered after the exchange / stage-in); a
+      // delayed worker "sleeps" on the host timer and only then computes.
       if (staged) stage_in({rank}, w.stream);
       else HIPCHECK(hipStreamWaitEvent(w.stream, xfer_ev_, 0));
-      if (delay > 0) HIPCHECK(launch_delay((unsigned long long)(double(delay) * 1e-9 * rt_hz_), w.stream));
+      std::function<void()> go;
       if (ts.kind == MPA_TASK_LSQ) {
-        launch_lsq_batch({rank}, ts.dtype, w.stream);
+        double bytes = 0;
+        const LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes);
+        const int cols = int(ts.cols), dt = ts.dtype;
+        hipStream_t s = w.stream;
+        go = [this, b, dt, cols, s, bytes]() { enqueue_lsq(b, dt, cols, s, bytes); };
       } else {
         KmapArgs a{};
         a.kind = ts.kind;
@@ -561,10 +577,105 @@ class HipComm final : public Comm {
         a.out = w.out;
         a.rl = w.rl;
         a.pub = Publish{w.flag_dev, err_dev_, w.seq, spin_ticks()};
-        HIPCHECK(launch_kmap(a, w.stream));
+        hipStream_t s = w.stream;
+        go = [a, s]() { HIPCHECK(launch_kmap(a, s)); };
       }
+      if (delay > 0) defer(mono_ns() + uint64_t(delay), std::move(go));
+      else go();
     }
     emit();
+  }
+
+  // ---- straggler emulation -------------------------------------------------------------
+  // A worker with a delay schedule sleeps `delay` ns after its message is delivered and
+  // then computes (the reference worker's `sleep(rand())` before its reply,
+  // examples/iterative_example.jl:74).  The sleep is a host timer thread that launches the
+  // task kernel when it is due, so a sleeping worker holds no GPU queue: kernels parked
+  // in queues (a spinning delay kernel) made one straggler hold back another once the
+  // process had more streams than the GPU maps hardware queues for.
+  static uint64_t mono_ns() {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count());
+  }
+
+  struct Deferred {
+    uint64_t due;
+    std::function<void()> go;
+    bool operator<(const Deferred& o) const { return due > o.due; }  // min-heap on due
+  };
+
+  void defer(uint64_t due, std::function<void()> go) {
+    std::lock_guard<std::mutex> lk(tmu_);
+    if (!timer_.joinable()) {
+      tstop_ = false;
+      timer_ = std::thread([this]() { timer_loop(); });
+    }
+    deferred_.push_back(Deferred{due, std::move(go)});
+    std::push_heap(deferred_.begin(), deferred_.end());
+    tcv_.notify_all();
+  }
+
+  void timer_loop() {
+    (void)hipSetDevice(dev_);
+    std::unique_lock<std::mutex> lk(tmu_);
+    for (;;) {
+      if (tstop_) break;
+      if (deferred_.empty()) {
+        tidle_.notify_all();
+        tcv_.wait(lk);
+        continue;
+      }
+      const uint64_t due = deferred_.front().due, now = mono_ns();
+      if (now + 200000 < due) {  // sleep to ~100 us before the deadline, then spin
+        tcv_.wait_for(lk, std::chrono::nanoseconds(due - now - 100000));
+        continue;
+      }
+      if (now < due) {
+        lk.unlock();
+        while (mono_ns() < due) __builtin_ia32_pause();
+        lk.lock();
+        continue;
+      }
+      std::pop_heap(deferred_.begin(), deferred_.end());
+      Deferred d = std::move(deferred_.back());
+      deferred_.pop_back();
+      tbusy_ = true;
+      lk.unlock();
+      try {
+        d.go();
+      } catch (const Failure&) {
+        std::lock_guard<std::mutex> g(tfail_mu_);
+        if (tfail_msg_.empty()) tfail_msg_ = last_error();  // this thread's error text
+        tfailed_.store(true, std::memory_order_release);
+      }
+      lk.lock();
+      tbusy_ = false;
+    }
+  }
+
+  // every deferred launch issued (shutdown)
+  void drain_deferred() {
+    std::unique_lock<std::mutex> lk(tmu_);
+    if (!timer_.joinable()) return;
+    tidle_.wait(lk, [this]() { return (deferred_.empty() && !tbusy_) || tstop_; });
+  }
+
+  // pending launches are dropped (the comm is being destroyed)
+  void stop_timer() {
+    {
+      std::lock_guard<std::mutex> lk(tmu_);
+      tstop_ = true;
+      deferred_.clear();
+      tcv_.notify_all();
+      tidle_.notify_all();
+    }
+    if (timer_.joinable()) timer_.join();
+  }
+
+  void check_timer() {
+    if (tfailed_.load(std::memory_order_acquire)) {
+      std::lock_guard<std::mutex> g(tfail_mu_);
+      fail(MPA_DEVICE_ERROR, "deferred task launch failed: %s", tfail_msg_.c_str());
+    }
   }
 
   void stage_in(const std::vector<int64_t>& ranks, hipStream_t s) {
@@ -619,6 +730,13 @@ class HipComm final : public Comm {
   }
 
   void launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hipStream_t s) {
+    double bytes = 0;
+    const LsqBatch b = build_lsq_batch(ranks, dtype, &bytes);
+    enqueue_lsq(b, dtype, int(tasks_[size_t(ranks[0] - 1)].cols), s, bytes);
+  }
+
+  // kernel arguments of one launch over `ranks`; advances their arrival-counter bases
+  LsqBatch build_lsq_batch(const std::vector<int64_t>& ranks, int dtype, double* bytes_out) {
     LsqBatch b{};
     b.ntasks = int(ranks.size());
     b.err = err_dev_;
@@ -642,25 +760,36 @@ class HipComm final : public Comm {
       t.lda = ts.lda;
       t.cols = int(ts.cols);
       t.grid = lsq_grid(ts, w, b.ntasks);
+      t.base0 = w.ctr0;
+      t.base1 = w.ctr1;
+      w.ctr0 += uint32_t(t.grid);
+      w.ctr1 += uint32_t(lsq_reducers(ts.dtype, int(ts.cols)));
       b.block0[k] = blocks;
       blocks += t.grid;
       const double es = dtype == MPA_F64 ? 8.0 : 4.0;
       bytes += es * (double(ts.rows) * double(ts.cols) + double(ts.rows) + 2.0 * double(ts.cols));
     }
     b.block0[b.ntasks] = blocks;
+    *bytes_out = bytes;
+    return b;
+  }
+
+  // enqueue one least-squares launch on `s` (coordinator / server thread or timer thread)
+  void enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes) {
     TimedLaunch tl{};
-    if (timing_) {
+    const bool timed = timing_;
+    if (timed) {
+      std::lock_guard<std::mutex> lk(tm_mu_);
       tl.start = take_event();
       tl.stop = take_event();
       tl.bytes = bytes;
-      HIPCHECK(hipEventRecord(tl.start, s));
     }
+    if (timed) HIPCHECK(hipEventRecord(tl.start, s));
     if (debug_) {
       for (int k = 0; k < b.ntasks; ++k) {
         const LsqTask& t = b.t[k];
-        std::fprintf(stderr, "[mpa role %d] lsq task %lld seq %llu grid %d A %p b %p x %p out %p slab %p ctr %p flag %p\n",
-                     int(role_), (long long)ranks[size_t(k)], t.seq, t.grid, t.A, t.b, t.x, t.out, t.slab, (void*)t.ctr,
-                     (void*)t.flag);
+        std::fprintf(stderr, "[mpa role %d] lsq task seq %llu grid %d A %p b %p x %p out %p slab %p ctr %p flag %p\n",
+                     int(role_), t.seq, t.grid, t.A, t.b, t.x, t.out, t.slab, (void*)t.ctr, (void*)t.flag);
         describe("A", t.A);
         describe("x", t.x);
         describe("out", t.out);
@@ -668,14 +797,15 @@ class HipComm final : public Comm {
       }
       std::fflush(stderr);
     }
-    HIPCHECK(launch_lsq(dtype, int(tasks_[size_t(ranks[0] - 1)].cols), b, s));
+    HIPCHECK(launch_lsq(dtype, cols, b, s));
     if (debug_) {
       const hipError_t e = hipStreamSynchronize(s);
       std::fprintf(stderr, "[mpa role %d] lsq launch done: %s\n", int(role_), hipGetErrorString(e));
       std::fflush(stderr);
     }
-    if (timing_) {
+    if (timed) {
       HIPCHECK(hipEventRecord(tl.stop, s));
+      std::lock_guard<std::mutex> lk(tm_mu_);
       timed_.push_back(tl);
     }
   }
@@ -715,6 +845,7 @@ class HipComm final : public Comm {
   }
 
   void reap_timing(bool block) {
+    std::lock_guard<std::mutex> lk(tm_mu_);
     size_t keep = 0;
     for (size_t k = 0; k < timed_.size(); ++k) {
       TimedLaunch& tl = timed_[k];
@@ -761,6 +892,16 @@ class HipComm final : public Comm {
   double t_ms_ = 0, t_bytes_ = 0;
   std::vector<hipStream_t> launch_streams_;
   size_t next_launch_ = 0;
+  std::mutex tm_mu_;  // timed_ / event_pool_ (the timer thread also launches)
+  // straggler timer thread
+  std::thread timer_;
+  std::mutex tmu_;
+  std::condition_variable tcv_, tidle_;
+  std::vector<Deferred> deferred_;
+  bool tstop_ = false, tbusy_ = false;
+  std::atomic<bool> tfailed_{false};
+  std::mutex tfail_mu_;
+  std::string tfail_msg_;
 
  public:
   void init_ticket() { ticket_ = ctr_ + 2 * nworkers_; }

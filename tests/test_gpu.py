@@ -159,7 +159,7 @@ def _warm_kernels(M, torch, n):
     comm.close()
 
 
-def test_delay_kernel_calibration(M, torch_mod):
+def test_delay_calibration(M, torch_mod):
     """An injected delay of d ms shows up as a latency of d ms (+ < 1 ms dispatch)."""
     torch = torch_mod
     _warm_kernels(M, torch, 2)
