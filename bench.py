@@ -183,6 +183,9 @@ def run_single(args, cfg):
              "python_loop_it_per_s": round(args.steps / el_py, 3)}
     extra["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(cfg, args.cpu_seconds)
     print(json.dumps(report(args, cfg, 1, el, kl, kms, kbytes, extra)), flush=True)
+    comm.shutdown()
+    comm.close()
+    torch.cuda.synchronize()
 
 
 def run_multi(args, cfg, rank, world, local):
