@@ -37,6 +37,19 @@ CONFIGS = {
     "c2": dict(rows=1 << 20, cols=1024, workers=8, nwait=8, dtype="f32",
                desc="BASELINE configs[1]: fp32 least squares A 2^20x1024 row-sharded over 8 logical workers, "
                     "nwait=8 (no stragglers); 1 GPU = 8 stream-workers, N GPUs = 8/N workers per GPU"),
+    # the other BASELINE configs at their full global size, 8 workers on ONE GPU (secondary
+    # measurements and parity cases; the default bench line is c2)
+    "c3": dict(rows=1 << 23, cols=2048, workers=8, nwait=6, dtype="f32", delay_mean_ms=1.0,
+               desc="BASELINE configs[2] shape on one GPU: fp32 A 2^23x2048 (8 GiB per worker), nwait=6, "
+                    "injected Exp(1 ms) straggler delays per (worker, task)"),
+    "c4": dict(rows=1 << 23, cols=2048, workers=8, nwait="worker1+5", dtype="f64", delay_mean_ms=1.0,
+               stale_weight=0.5,
+               desc="BASELINE configs[3] shape on one GPU: fp64 A 2^23x2048 (16 GiB per worker), nwait = "
+                    "worker 1 fresh + 5 others (test/kmap2.jl:65 style predicate), stale results folded in "
+                    "at weight 0.5, Exp(1 ms) delays"),
+    "c5": dict(rows=1 << 23, cols=2048, workers=8, nwait=7, dtype="bf16", iterates=64,
+               desc="BASELINE configs[4] shape on one GPU: batched 64-iterate variant, bf16 A 2^23x2048 "
+                    "(4 GiB per worker), X 2048x64, fp32 accumulate (MFMA), nwait=7"),
 }
 
 
@@ -79,15 +92,37 @@ def step_size(rows, cols):
     return 0.9 / L
 
 
+TORCH_DT = {"f32": "float32", "f64": "float64", "bf16": "bfloat16"}
+
+
 def gen_shard(M, torch, cfg, seed, w):
-    """Rows of worker w (1-based) of the global synthetic problem, on the current GPU."""
+    """Rows of worker w (1-based) of the global synthetic problem, on the current GPU
+    (b: rows; the batched variant's B: rows x 64)."""
     n, rows, cols = cfg["workers"], cfg["rows"], cfg["cols"]
     per = rows // n
-    A = torch.empty(per, cols, dtype=torch.float32, device="cuda")
-    b = torch.empty(per, dtype=torch.float32, device="cuda")
-    M.generate(A, seed, 0, (w - 1) * per * cols, float(np.float32(1.0 / np.sqrt(cols))))
-    M.generate(b, seed, 1, (w - 1) * per, 1.0)
+    dt = getattr(torch, TORCH_DT[cfg["dtype"]])
+    k = cfg.get("iterates", 1)
+    A = torch.empty(per, cols, dtype=dt, device="cuda")
+    b = torch.empty((per, k) if k > 1 else per, dtype=dt, device="cuda")
+    scale = 1.0 / np.sqrt(cols) if cfg["dtype"] == "f64" else float(np.float32(1.0 / np.sqrt(cols)))
+    M.generate(A, seed, 0, (w - 1) * per * cols, scale)
+    M.generate(b, seed, 1, (w - 1) * per * k, 1.0)
     return A, b
+
+
+def delay_schedule(cfg, seed, w, count=4096):
+    """Exp(mean) straggler delay per (worker, task), seeded (stored with the results)."""
+    mean = cfg.get("delay_mean_ms")
+    if not mean:
+        return None
+    rng = np.random.default_rng([seed, w])
+    return (rng.exponential(mean * 1e6, size=count)).astype(np.int64)
+
+
+def kernel_name(cfg):
+    if cfg.get("iterates", 1) > 1:
+        return "lsqb_resid_kernel + lsqb_grad_kernel (bf16 MFMA, two launches per batch)"
+    return "lsq_grad_kernel (one batched launch per epoch per GPU)"
 
 
 def report(args, cfg, world, el, kl, kms, kbytes, extra):
@@ -97,12 +132,21 @@ def report(args, cfg, world, el, kl, kms, kbytes, extra):
     per_launch_s = kms / 1e3 / max(kl, 1)
     achieved = per_launch_bytes / per_launch_s / 1e9 if kl else None
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "lsq_pmc_c2.json")
+    pmc = os.path.join(ROOT, "profiles", f"lsq_pmc_{cfg['config']}.json")
     if os.path.exists(pmc) and world == 1:
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    es = {"f32": 4, "f64": 8, "bf16": 2}[cfg["dtype"]]
+    k = cfg.get("iterates", 1)
+    epoch_bytes = es * (rows * cols + rows * k) + n * cols * k * (es + (4 if k > 1 else es))
+    cfg_out = {"workload": cfg["desc"], "rows": rows, "cols": cols, "workers": n, "nwait": cfg["nwait"],
+               "shard_bytes": rows // n * cols * es, "parallelism": f"{n} logical workers on {world} GPU(s)"}
+    if k > 1:
+        cfg_out["iterates"] = k
+    if cfg.get("delay_mean_ms"):
+        cfg_out["delays"] = f"Exp(mean {cfg['delay_mean_ms']} ms) per (worker, task), seed {args.seed}"
     out = {
         "metric": METRIC,
         "value": round(its, 3),
@@ -114,21 +158,27 @@ def report(args, cfg, world, el, kl, kms, kbytes, extra):
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": cfg["dtype"],
         "data": "synthetic (Philox4x32-10 generated on device, DESIGN.md §Data)",
-        "config": {"workload": cfg["desc"], "rows": rows, "cols": cols, "workers": n, "nwait": cfg["nwait"],
-                   "shard_bytes": rows // n * cols * 4, "parallelism": f"{n} logical workers on {world} GPU(s)"},
+        "config": cfg_out,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
                      "traffic": traffic,
-                     "kernel": "lsq_grad_kernel (one batched launch per epoch per GPU)",
+                     "kernel": kernel_name(cfg),
                      "alg_bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4),
                      "launches": kl},
-        "epoch_alg_GBps": round(4.0 * (rows * cols + rows + 2 * n * cols) * its / 1e9, 1),
+        "epoch_alg_GBps": round(epoch_bytes * its / 1e9, 1),
     }
     out.update(extra)
     return out
+
+
+def _nwait(M, cfg):
+    nw = cfg["nwait"]
+    if isinstance(nw, str) and nw.startswith("worker1+"):
+        return M.first_plus(int(nw.split("+")[1]))
+    return nw
 
 
 def run_single(args, cfg):
@@ -136,52 +186,80 @@ def run_single(args, cfg):
     import mpiasyncpools as M
 
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    n, cols, nwait = cfg["workers"], cfg["cols"], cfg["nwait"]
+    n, cols = cfg["workers"], cfg["cols"]
+    nwait = _nwait(M, cfg)
+    k = cfg.get("iterates", 1)
+    batched = k > 1
     comm = M.DeviceComm(n)
     shards = [gen_shard(M, torch, cfg, args.seed, w) for w in range(1, n + 1)]
     for w, (A, b) in enumerate(shards, start=1):
-        comm.set_task_lsq(w, A, b)
+        if batched:
+            comm.set_task_lsq_batch(w, A, b)
+        else:
+            comm.set_task_lsq(w, A, b)
+        d = delay_schedule(cfg, args.seed, w)
+        if d is not None:
+            comm.set_delays(w, d)
     pool = M.MPIAsyncPool(n)
-    x = torch.zeros(cols, device="cuda")
-    isend = torch.zeros(n * cols, device="cuda")
-    recv = torch.zeros(n * cols, device="cuda")
-    irecv = torch.zeros_like(recv)
     eta = step_size(cfg["rows"], cols)
-    w = np.zeros(n)
+    stale = cfg.get("stale_weight", 0.0)
+    if batched:
+        x = torch.zeros(cols * k, device="cuda")          # fp32 master iterate X (cols x 64)
+        xb = torch.zeros(cols * k, dtype=torch.bfloat16, device="cuda")  # its bf16 message
+        isend = torch.zeros(n * cols * k, dtype=torch.bfloat16, device="cuda")
+        recv = torch.zeros(n * cols * k, device="cuda")
 
-    def step():
-        rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=nwait)
-        fresh = rep == pool.epoch
-        nf = int(fresh.sum())
-        w[:] = fresh * (n / nf if nf else 0.0)
-        comm.lsq_update(x, recv, n, w, eta)
+        def loop(steps):
+            M.lsqb_descent(pool, comm, x, xb, recv, isend, irecv, nwait, eta, steps, stale_weight=stale)
+    else:
+        dt = getattr(torch, TORCH_DT[cfg["dtype"]])
+        x = torch.zeros(cols, dtype=dt, device="cuda")
+        isend = torch.zeros(n * cols, dtype=dt, device="cuda")
+        recv = torch.zeros(n * cols, dtype=dt, device="cuda")
 
-    # the same loop from Python (asyncmap_ + weights + lsq_update per step), reported beside
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    el_py = time.perf_counter() - t0
-    # timed region: the coordinator loop in native code (mpa_lsq_descent: the same calls)
-    M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, eta, args.warmup)
+        def loop(steps):
+            M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, eta, steps, stale_weight=stale)
+    irecv = torch.zeros_like(recv)
+    extra = {}
+    if cfg["config"] == "c2":
+        # the same loop from Python (asyncmap_ + weights + lsq_update per step), reported beside
+        w = np.zeros(n)
+
+        def step():
+            rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=nwait)
+            fresh = rep == pool.epoch
+            nf = int(fresh.sum())
+            w[:] = fresh * (n / nf if nf else 0.0)
+            comm.lsq_update(x, recv, n, w, eta)
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        extra["python_loop_it_per_s"] = round(args.steps / (time.perf_counter() - t0), 3)
+    # timed region: the coordinator loop in native code (mpa_lsq_descent / mpa_lsqb_descent)
+    loop(args.warmup)
     torch.cuda.synchronize()
     comm.timing()
     comm.set_timing(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, eta, args.steps)
+    loop(args.steps)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     kl, kms, kbytes = comm.timing()
     comm.set_timing(False)
+    fresh = int((pool.repochs == pool.epoch).sum())
     M.waitall_(pool, recv, irecv)
-    extra = {"x_norm": float(torch.linalg.norm(x).item()), "build": M.lib().mpa_build_info().decode(),
-             "loop": "native coordinator loop (mpa_lsq_descent); python loop beside it",
-             "python_loop_it_per_s": round(args.steps / el_py, 3)}
-    extra["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(cfg, args.cpu_seconds)
+    extra.update({"x_norm": float(torch.linalg.norm(x.float()).item()), "build": M.lib().mpa_build_info().decode(),
+                  "loop": "native coordinator loop (mpa_lsq%s_descent)" % ("b" if batched else ""),
+                  "fresh_at_last_epoch": fresh})
+    if cfg["config"] == "c2":
+        extra["loop"] += "; python loop beside it"
+    extra["cpu_baseline"] = None if (args.no_cpu_baseline or cfg["config"] != "c2") else cpu_baseline(cfg, args.cpu_seconds)
     print(json.dumps(report(args, cfg, 1, el, kl, kms, kbytes, extra)), flush=True)
     comm.shutdown()
     comm.close()

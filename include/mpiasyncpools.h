@@ -93,6 +93,11 @@ enum mpa_task {
  * Return 1 (true), 0 (false) or a negative value if the callback raised. */
 typedef int (*mpa_nwait_fn)(void* ctx, int64_t epoch, const int64_t* repochs, int64_t n);
 
+/* A ready-made native nwait predicate (BASELINE configs[3]): true when worker 1 is fresh
+ * (repochs[0] == epoch, the predicate of test/kmap2.jl:65) and at least *(int64_t*)ctx of
+ * the other workers are fresh too. */
+int mpa_nwait_first_plus(void* ctx, int64_t epoch, const int64_t* repochs, int64_t n);
+
 int mpa_abi_version(void);
 const char* mpa_last_error(void);
 /* build description: target arch and the least-squares kernel variant in use */
@@ -152,6 +157,12 @@ int mpa_comm_set_task_kmap(mpa_comm* comm, int64_t rank, int task /* ECHO/KMAP1/
  * g_i = cols elements, dtype MPA_F32 or MPA_F64. */
 int mpa_comm_set_task_lsq(mpa_comm* comm, int64_t rank, int dtype, int64_t rows, int64_t cols,
                           const void* A, int64_t lda, const void* b);
+/* the batched multi-iterate variant (BASELINE configs[4]): G_i = A_i^T (A_i X - B_i) with
+ * A_i rows x cols bf16 (leading dimension lda, lda % 8 == 0, 16-byte aligned), B_i rows x k
+ * bf16 (row-major), the message X = cols x k bf16 and the reply G_i = cols x k fp32, both
+ * row-major; k == 64, cols % 32 == 0, cols <= 4096.  bf16 MFMA with fp32 accumulation. */
+int mpa_comm_set_task_lsq_batch(mpa_comm* comm, int64_t rank, int64_t rows, int64_t cols, int64_t k,
+                                const void* A, int64_t lda, const void* B);
 /* straggler emulation: task t (1-based) of the worker is delayed by
  * delays_ns[(t-1) % count] before it computes; count == 0 clears the schedule */
 int mpa_comm_set_delays(mpa_comm* comm, int64_t rank, const int64_t* delays_ns, int64_t count);
@@ -204,6 +215,18 @@ int mpa_lsq_update(mpa_comm* comm, int dtype, void* x, const void* recvbuf, int6
 int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols, void* recvbuf,
                     void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
                     void* nwait_ctx, double eta, double stale_weight, int64_t epochs);
+
+/* The batched multi-iterate variant (mpa_comm_set_task_lsq_batch): the iterate X (cols x 64)
+ * is kept as an fp32 master x32 and sent as its bf16 rounding xb16 (the message);
+ *     x32 -= eta * sum_i weights[i] * G_i ;  xb16 = bf16(x32)        (one device kernel)
+ * elems = cols * 64; recvbuf holds nchunks fp32 chunks of elems. */
+int mpa_lsqb_update(mpa_comm* comm, void* x32, void* xb16, const void* recvbuf, int64_t nchunks, int64_t elems,
+                    const double* weights, double eta);
+/* mpa_lsq_descent for the batched variant: sendbuf = xb16 (elems bf16), recvbuf /
+ * irecvbuf n * elems fp32, isendbuf n * elems bf16, update by mpa_lsqb_update. */
+int mpa_lsqb_descent(mpa_pool* pool, mpa_comm* comm, void* x32, void* xb16, int64_t elems, void* recvbuf,
+                     void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
+                     void* nwait_ctx, double eta, double stale_weight, int64_t epochs);
 
 /* ---- synthetic data (device): Philox4x32-10 layout of DESIGN.md §Data ------------- */
 /* out[k] = unit(philox(seed, stream, e0 + k)) * scale, k < count, dtype F32/F64/BF16 */

@@ -236,6 +236,32 @@ int mpa_comm_set_task_lsq(mpa_comm* comm, int64_t rank, int dtype, int64_t rows,
   });
 }
 
+int mpa_comm_set_task_lsq_batch(mpa_comm* comm, int64_t rank, int64_t rows, int64_t cols, int64_t k, const void* A,
+                                int64_t lda, const void* B) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    if (rows < 0 || cols <= 0 || k <= 0) mpa::fail(MPA_ARGUMENT_ERROR, "batched least squares: bad shape");
+    if (rows > 0 && (!A || !B)) mpa::fail(MPA_ARGUMENT_ERROR, "batched least squares: A and B must be device pointers");
+    mpa::TaskSpec& t = c.task(rank);
+    const mpa::TaskSpec saved = t;
+    t.kind = MPA_TASK_LSQ_BATCH;
+    t.dtype = MPA_BF16;
+    t.rows = rows;
+    t.cols = cols;
+    t.k = k;
+    t.lda = lda;
+    t.A = A;
+    t.b = B;
+    try {
+      c.on_task_changed(rank);
+    } catch (...) {
+      t = saved;
+      throw;
+    }
+  });
+}
+
 int mpa_comm_set_delays(mpa_comm* comm, int64_t rank, const int64_t* delays_ns, int64_t count) {
   return guarded([&] {
     mpa::Comm& c = comm_of(comm);
@@ -299,7 +325,7 @@ int64_t mpa_comm_sim_now(const mpa_comm* comm) {
 }
 
 static int aggregate_impl(mpa_comm* comm, int dtype, const void* recvbuf, int64_t n, int64_t elems,
-                          const double* weights, void* out, int update, double eta) {
+                          const double* weights, void* out, int update, double eta, void* mirror = nullptr) {
   return guarded([&] {
     mpa::Comm& c = comm_of(comm);
     need_hip(c);
@@ -315,6 +341,7 @@ static int aggregate_impl(mpa_comm* comm, int dtype, const void* recvbuf, int64_
     a.stride = elems;
     a.eta = eta;
     a.update = update;
+    a.mirror = static_cast<uint16_t*>(mirror);
     for (int64_t i = 0; i < n; ++i) a.w[i] = weights[i];
     HIPCHECK_C(mpa::launch_aggregate(dtype, a, static_cast<hipStream_t>(mpa::hip_get_stream(&c))));
   });
@@ -330,23 +357,22 @@ int mpa_lsq_update(mpa_comm* comm, int dtype, void* x, const void* recvbuf, int6
   return aggregate_impl(comm, dtype, recvbuf, nchunks, cols, weights, x, 1, eta);
 }
 
-int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols, void* recvbuf, void* isendbuf,
-                    void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn, void* nwait_ctx, double eta,
-                    double stale_weight, int64_t epochs) {
-  int rc = guarded([&] {
-    if (!pool) mpa::fail(MPA_ARGUMENT_ERROR, "pool is NULL");
-    if (dtype != MPA_F32 && dtype != MPA_F64) mpa::fail(MPA_ARGUMENT_ERROR, "lsq_descent: dtype must be F32 or F64");
-    if (cols <= 0 || epochs < 0) mpa::fail(MPA_ARGUMENT_ERROR, "lsq_descent: bad cols / epochs");
-  });
-  if (rc != MPA_OK) return rc;
+}  // extern "C"
+namespace {
+// The coordinator loop shared by mpa_lsq_descent / mpa_lsqb_descent: `epochs` iterations of
+// asyncmap! followed by the iterate update (examples/iterative_example.jl:37-47).
+template <typename Update>
+int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_bytes, int64_t elems, size_t reply_es,
+                 void* recvbuf, void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
+                 void* nwait_ctx, double stale_weight, int64_t epochs, Update update) {
   mpa::Pool& p = pool->p;
   const int64_t n = p.n;
-  const size_t es = dtype == MPA_F64 ? 8 : 4;
-  const size_t sl = size_t(cols) * es, tot = size_t(n) * sl;
+  const size_t rl = size_t(elems) * reply_es;
   std::vector<double> w(static_cast<size_t>(n), 0.0);
   for (int64_t e = 0; e < epochs; ++e) {
-    rc = mpa_asyncmap(pool, x, sl, recvbuf, tot, size_t(n * cols), isendbuf, tot, irecvbuf, tot, comm, nwait_kind,
-                      nwait, nwait_fn, nwait_ctx, "Int64", p.epoch + 1, 0, nullptr);
+    int rc = mpa_asyncmap(pool, msg, msg_bytes, recvbuf, size_t(n) * rl, size_t(n * elems), isendbuf,
+                          size_t(n) * msg_bytes, irecvbuf, size_t(n) * rl, comm, nwait_kind, nwait, nwait_fn, nwait_ctx,
+                          "Int64", p.epoch + 1, 0, nullptr);
     if (rc != MPA_OK) return rc;
     double sum = 0;
     for (int64_t i = 0; i < n; ++i) {
@@ -357,10 +383,57 @@ int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t 
     }
     const double s = sum > 0 ? double(n) / sum : 0.0;
     for (auto& v : w) v *= s;
-    rc = mpa_lsq_update(comm, dtype, x, recvbuf, n, cols, w.data(), eta);
+    rc = update(w.data());
     if (rc != MPA_OK) return rc;
   }
   return MPA_OK;
+}
+}  // namespace
+extern "C" {
+
+int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols, void* recvbuf, void* isendbuf,
+                    void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn, void* nwait_ctx, double eta,
+                    double stale_weight, int64_t epochs) {
+  int rc = guarded([&] {
+    if (!pool) mpa::fail(MPA_ARGUMENT_ERROR, "pool is NULL");
+    if (dtype != MPA_F32 && dtype != MPA_F64) mpa::fail(MPA_ARGUMENT_ERROR, "lsq_descent: dtype must be F32 or F64");
+    if (cols <= 0 || epochs < 0) mpa::fail(MPA_ARGUMENT_ERROR, "lsq_descent: bad cols / epochs");
+  });
+  if (rc != MPA_OK) return rc;
+  const size_t es = dtype == MPA_F64 ? 8 : 4;
+  const int64_t n = pool->p.n;
+  return descent_loop(pool, comm, x, size_t(cols) * es, cols, es, recvbuf, isendbuf, irecvbuf, nwait_kind, nwait,
+                      nwait_fn, nwait_ctx, stale_weight, epochs,
+                      [&](const double* w) { return mpa_lsq_update(comm, dtype, x, recvbuf, n, cols, w, eta); });
+}
+
+int mpa_nwait_first_plus(void* ctx, int64_t epoch, const int64_t* repochs, int64_t n) {
+  if (!ctx || !repochs || n <= 0) return -1;
+  const int64_t k = *static_cast<const int64_t*>(ctx);
+  if (repochs[0] != epoch) return 0;
+  int64_t fresh = 0;
+  for (int64_t i = 1; i < n; ++i) fresh += repochs[i] == epoch;
+  return fresh >= k ? 1 : 0;
+}
+
+int mpa_lsqb_update(mpa_comm* comm, void* x32, void* xb16, const void* recvbuf, int64_t nchunks, int64_t elems,
+                    const double* weights, double eta) {
+  if (!xb16) return guarded([&] { mpa::fail(MPA_ARGUMENT_ERROR, "lsqb_update: the bf16 iterate is NULL"); });
+  return aggregate_impl(comm, MPA_F32, recvbuf, nchunks, elems, weights, x32, 1, eta, xb16);
+}
+
+int mpa_lsqb_descent(mpa_pool* pool, mpa_comm* comm, void* x32, void* xb16, int64_t elems, void* recvbuf,
+                     void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
+                     void* nwait_ctx, double eta, double stale_weight, int64_t epochs) {
+  int rc = guarded([&] {
+    if (!pool) mpa::fail(MPA_ARGUMENT_ERROR, "pool is NULL");
+    if (!x32 || !xb16 || elems <= 0 || epochs < 0) mpa::fail(MPA_ARGUMENT_ERROR, "lsqb_descent: bad arguments");
+  });
+  if (rc != MPA_OK) return rc;
+  const int64_t n = pool->p.n;
+  return descent_loop(pool, comm, xb16, size_t(elems) * 2, elems, 4, recvbuf, isendbuf, irecvbuf, nwait_kind, nwait,
+                      nwait_fn, nwait_ctx, stale_weight, epochs,
+                      [&](const double* w) { return mpa_lsqb_update(comm, x32, xb16, recvbuf, n, elems, w, eta); });
 }
 
 int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count, double scale,

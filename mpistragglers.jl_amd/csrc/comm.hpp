@@ -31,8 +31,9 @@ struct TaskSpec {
   int kind = MPA_TASK_NONE;
   int dtype = MPA_F32;
   int64_t rows = 0, cols = 0, lda = 0;
+  int64_t k = 1;  // iterates per message (MPA_TASK_LSQ_BATCH: kLsqbIterates)
   const void* A = nullptr;
-  const void* b = nullptr;
+  const void* b = nullptr;  // b (rows) or B (rows x k)
   std::vector<int64_t> delays_ns;
 };
 

@@ -86,6 +86,11 @@ __global__ void __launch_bounds__(64) kmap_task_kernel(KmapArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return uint16_t((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kThreads) aggregate_kernel(AggregateArgs a) {
   const T* c = static_cast<const T*>(a.chunks);
@@ -95,7 +100,9 @@ __global__ void __launch_bounds__(kThreads) aggregate_kernel(AggregateArgs a) {
     double s = 0.0;
     for (int64_t i = 0; i < a.n; ++i)
       if (a.w[i] != 0.0) s += a.w[i] * double(c[i * a.stride + j]);
-    out[j] = a.update ? T(double(out[j]) - a.eta * s) : T(s);
+    const T v = a.update ? T(double(out[j]) - a.eta * s) : T(s);
+    out[j] = v;
+    if (a.mirror) a.mirror[j] = f32_to_bf16_rne(float(v));
   }
 }
 
@@ -114,11 +121,6 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
 
 __device__ __forceinline__ float unit_f32(uint32_t w) {
   return float(int32_t(w >> 8) - 8388608) * (1.0f / 8388608.0f);
-}
-
-__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return uint16_t((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
 }
 
 __global__ void __launch_bounds__(kThreads) generate_kernel(void* out, int dtype, uint64_t seed, uint32_t stream,

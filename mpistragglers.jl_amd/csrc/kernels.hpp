@@ -75,6 +75,38 @@ int lsq_cols_pad(int dtype, int cols);  // 0 if unsupported
 int lsq_reducers(int dtype, int cols);
 int lsq_rows_per_wave_iter(int dtype, int cols);
 
+// One worker task of the batched multi-iterate variant (lsqb_kernel.hip):
+// G = A^T (A X - B), A rows x cols bf16 (lda), X cols x 64 bf16 (the message, row-major),
+// B rows x 64 bf16, G cols x 64 fp32 (the reply, row-major).
+constexpr int kLsqbIterates = 64;
+constexpr int kLsqbMaxSlices = 16;  // 256-column slices: cols <= 4096
+struct LsqbTask {
+  const void* A;
+  const void* B;
+  const void* X;
+  void* out;
+  void* R;      // [rows_pad/8][64][hi 8 | lo 8] bf16 residual (pass 1 -> pass 2)
+  void* slab;   // [nrange][nslice][64 x 256] fp32 partials of pass 2
+  uint32_t* ctr;  // [kLsqbMaxSlices] per-slice arrivals + [1] per-task slice completions
+  unsigned long long* flag;
+  unsigned long long seq;
+  int64_t rows, lda;
+  int cols;
+  int grid1;           // pass-1 workgroups (256 rows each, grid-strided)
+  int nrange, nslice;  // pass-2 grid = nrange * nslice
+  uint32_t sbase, tbase;  // ctr values before this launch (every slice counter moves alike)
+};
+struct LsqbBatch {
+  int ntasks;
+  unsigned* err;
+  unsigned long long spin_ticks;
+  int block1[kMaxLsqTasks + 1];
+  int block2[kMaxLsqTasks + 1];
+  LsqbTask t[kMaxLsqTasks];
+};
+// pass 1 + pass 2 of every task of the batch, two launches on `s`
+hipError_t launch_lsqb(const LsqbBatch& a, hipStream_t s);
+
 struct KmapArgs {
   int kind;
   double rank;
@@ -94,6 +126,7 @@ struct AggregateArgs {
   int64_t n, elems, stride;
   double eta;
   int update;
+  uint16_t* mirror;  // update only: bf16 copy of the updated fp32 out (the batched variant's X)
   double w[kMaxAggregate];
 };
 hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s);

@@ -60,6 +60,11 @@ using Clock = std::chrono::steady_clock;
 constexpr int kDefaultLaunchGrid = 512;  // 2 workgroups per CU: profiles/r01_tune_sweep2.jsonl
 constexpr int kSlabGridCap = 1024;       // most workgroups a single task may be given
 constexpr int kLaunchStreams = 2;
+// batched multi-iterate task: pass-1 / pass-2 workgroups per launch (resident: 2 / 4 per
+// CU by VGPRs), and the most row ranges a pass-2 task is split into
+constexpr int kLsqbGrid1 = 512;
+constexpr int kLsqbGrid2 = 1024;
+constexpr int kLsqbRangeCap = 128;
 
 // Process-wide pool of CU-masked streams: communicators come and go (tests create many),
 // but the HSA queues behind their streams are a bounded hardware resource, so a destroyed
@@ -102,6 +107,14 @@ struct HipWorker {
   void* slab = nullptr;
   int slab_grid = 0;
   uint32_t ctr0 = 0, ctr1 = 0;  // running totals of this worker's two arrival counters
+  // batched multi-iterate task (lsqb_kernel.hip): residual scratch, pass-2 partials,
+  // counters and their running totals
+  void* lsqb_R = nullptr;
+  size_t lsqb_R_bytes = 0;
+  void* lsqb_slab = nullptr;
+  size_t lsqb_slab_bytes = 0;
+  uint32_t* lsqb_ctr = nullptr;
+  uint32_t lsqb_sbase = 0, lsqb_tbase = 0;
   // current task
   int64_t slot = -1;
   const uint8_t* x = nullptr;
@@ -245,6 +258,9 @@ class HipComm final : public Comm {
     (void)hipDeviceSynchronize();
     for (auto& w : w_) {
       if (w.slab) (void)hipFree(w.slab);
+      if (w.lsqb_R) (void)hipFree(w.lsqb_R);
+      if (w.lsqb_slab) (void)hipFree(w.lsqb_slab);
+      if (w.lsqb_ctr) (void)hipFree(w.lsqb_ctr);
       if (w.xslot) (void)hipFree(w.xslot);
       if (w.stream) release_queue_stream(dev_, w.stream);
     }
@@ -397,6 +413,7 @@ class HipComm final : public Comm {
       fail(MPA_ERROR, "cannot change the task of worker %lld while it has an outstanding request", (long long)rank);
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
     if (ts.kind == MPA_TASK_LSQ) prepare_lsq(rank, ts);
+    if (ts.kind == MPA_TASK_LSQ_BATCH) prepare_lsqb(rank, ts);
   }
 
   // ---- worker process: watch the doorbells of the workers served here ----
@@ -488,6 +505,19 @@ class HipComm final : public Comm {
           fail(MPA_ARGUMENT_ERROR, "least-squares buffers must be %zu-byte aligned", es);
         return;
       }
+      case MPA_TASK_LSQ_BATCH: {
+        const size_t xb = size_t(ts.cols) * size_t(ts.k) * 2, gb = size_t(ts.cols) * size_t(ts.k) * 4;
+        if (sl < xb)
+          fail(MPA_DIMENSION_MISMATCH, "worker %lld (batched least squares, %lld x %lld bf16 X) needs %zu bytes of sendbuf, got %zu",
+               (long long)rank, (long long)ts.cols, (long long)ts.k, xb, sl);
+        if (rl < gb)
+          fail(MPA_DIMENSION_MISMATCH, "worker %lld (batched least squares) replies %zu bytes (fp32 G), recv chunk is %zu",
+               (long long)rank, gb, rl);
+        if (role_ != SERVER &&
+            ((reinterpret_cast<uintptr_t>(b_.isendbuf) | reinterpret_cast<uintptr_t>(b_.irecvbuf)) % 16 || sl % 16 || rl % 16))
+          fail(MPA_ARGUMENT_ERROR, "batched least-squares buffers and messages must be 16-byte aligned");
+        return;
+      }
       default:
         fail(MPA_ERROR, "worker %lld has no task registered (mpa_comm_set_task_*)", (long long)rank);
     }
@@ -513,6 +543,47 @@ class HipComm final : public Comm {
     }
   }
 
+  // batched multi-iterate task: validate, size the residual scratch / partial slab
+  void prepare_lsqb(int64_t rank, const TaskSpec& ts) {
+    HipWorker& w = w_[size_t(rank - 1)];
+    if (ts.k != kLsqbIterates)
+      fail(MPA_ARGUMENT_ERROR, "batched least squares: %d iterates per message are supported, got %lld", kLsqbIterates,
+           (long long)ts.k);
+    if (ts.cols <= 0 || ts.cols % 32 || ts.cols > 256 * kLsqbMaxSlices)
+      fail(MPA_ARGUMENT_ERROR, "batched least squares: cols (%lld) must be a positive multiple of 32, at most %d",
+           (long long)ts.cols, 256 * kLsqbMaxSlices);
+    if (ts.lda < ts.cols || ts.lda % 8)
+      fail(MPA_ARGUMENT_ERROR, "batched least squares: lda (%lld) must be >= cols and a multiple of 8", (long long)ts.lda);
+    if (reinterpret_cast<uintptr_t>(ts.A) % 16 || reinterpret_cast<uintptr_t>(ts.b) % 2)
+      fail(MPA_ARGUMENT_ERROR, "batched least squares: A must be 16-byte aligned and B element aligned");
+    if (ts.rows >= (int64_t(1) << 31)) fail(MPA_ARGUMENT_ERROR, "batched least squares: too many rows");
+    if (role_ == SERVER && size_t(ts.cols) * size_t(ts.k) * 4 > region_->max_msg())
+      fail(MPA_DIMENSION_MISMATCH, "batched least squares: %zu-byte replies exceed the mailbox",
+           size_t(ts.cols) * size_t(ts.k) * 4);
+    const size_t rows_pad = size_t((ts.rows + 255) / 256) * 256;
+    const size_t rbytes = std::max<size_t>(rows_pad * size_t(kLsqbIterates) * 4, 256);
+    if (rbytes > w.lsqb_R_bytes) {
+      if (w.lsqb_R) HIPCHECK(hipFree(w.lsqb_R));
+      w.lsqb_R = nullptr;
+      HIPCHECK(hipMalloc(&w.lsqb_R, rbytes));
+      w.lsqb_R_bytes = rbytes;
+    }
+    // pass-2 partials: [nrange][nslice][64 x 256 fp32]; nrange <= kLsqbRangeCap
+    const size_t nslice = size_t((ts.cols + 255) / 256);
+    const size_t sbytes = size_t(kLsqbRangeCap) * nslice * 256 * size_t(kLsqbIterates) * 4;
+    if (sbytes > w.lsqb_slab_bytes) {
+      if (w.lsqb_slab) HIPCHECK(hipFree(w.lsqb_slab));
+      w.lsqb_slab = nullptr;
+      HIPCHECK(hipMalloc(&w.lsqb_slab, sbytes));
+      w.lsqb_slab_bytes = sbytes;
+    }
+    if (!w.lsqb_ctr) {
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqb_ctr), sizeof(uint32_t) * (kLsqbMaxSlices + 1)));
+      HIPCHECK(hipMemset(w.lsqb_ctr, 0, sizeof(uint32_t) * (kLsqbMaxSlices + 1)));
+      HIPCHECK(hipDeviceSynchronize());
+    }
+  }
+
   // workgroups per task in a least-squares launch of `ntasks` tasks
   int lsq_grid(const TaskSpec& ts, const HipWorker& w, int ntasks) const {
     const int total = g_lsq_grid > 0 ? g_lsq_grid : kDefaultLaunchGrid;
@@ -534,14 +605,15 @@ class HipComm final : public Comm {
   // mailbox and is first copied into the worker's device slot on the launch's stream.
   void launch_tasks(const std::vector<int64_t>& ranks, bool staged) {
     std::vector<int64_t> batch;
-    int batch_dtype = -1, batch_cp = 0;
+    int batch_kind = -1, batch_dtype = -1, batch_cp = 0;
     hipStream_t bs = nullptr;
     auto emit = [&]() {
       if (batch.empty()) return;
       bs = pick_launch_stream();
       if (staged) stage_in(batch, bs);
       else HIPCHECK(hipStreamWaitEvent(bs, xfer_ev_, 0));
-      launch_lsq_batch(batch, batch_dtype, bs);
+      if (batch_kind == MPA_TASK_LSQ_BATCH) launch_lsqb_batch(batch, bs);
+      else launch_lsq_batch(batch, batch_dtype, bs);
       batch.clear();
     };
     for (int64_t rank : ranks) {
@@ -549,9 +621,12 @@ class HipComm final : public Comm {
       const TaskSpec& ts = tasks_[size_t(rank - 1)];
       int64_t delay = 0;
       if (!ts.delays_ns.empty()) delay = ts.delays_ns[size_t((int64_t(w.seq) - 1) % int64_t(ts.delays_ns.size()))];
-      if (ts.kind == MPA_TASK_LSQ && delay == 0) {
-        const int cp = lsq_cols_pad(ts.dtype, int(ts.cols));
-        if (!batch.empty() && (ts.dtype != batch_dtype || cp != batch_cp || batch.size() == size_t(kMaxLsqTasks))) emit();
+      if ((ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && delay == 0) {
+        const int cp = ts.kind == MPA_TASK_LSQ ? lsq_cols_pad(ts.dtype, int(ts.cols)) : 0;
+        if (!batch.empty() && (ts.kind != batch_kind || ts.dtype != batch_dtype || cp != batch_cp ||
+                               batch.size() == size_t(kMaxLsqTasks)))
+          emit();
+        batch_kind = ts.kind;
         batch_dtype = ts.dtype;
         batch_cp = cp;
         batch.push_back(rank);
@@ -568,6 +643,11 @@ class HipComm final : public Comm {
         const int cols = int(ts.cols), dt = ts.dtype;
         hipStream_t s = w.stream;
         go = [this, b, dt, cols, s, bytes]() { enqueue_lsq(b, dt, cols, s, bytes); };
+      } else if (ts.kind == MPA_TASK_LSQ_BATCH) {
+        double bytes = 0;
+        const LsqbBatch b = build_lsqb_batch({rank}, &bytes);
+        hipStream_t s = w.stream;
+        go = [this, b, s, bytes]() { enqueue_lsqb(b, s, bytes); };
       } else {
         KmapArgs a{};
         a.kind = ts.kind;
@@ -772,6 +852,82 @@ class HipComm final : public Comm {
     b.block0[b.ntasks] = blocks;
     *bytes_out = bytes;
     return b;
+  }
+
+  void launch_lsqb_batch(const std::vector<int64_t>& ranks, hipStream_t s) {
+    double bytes = 0;
+    const LsqbBatch b = build_lsqb_batch(ranks, &bytes);
+    enqueue_lsqb(b, s, bytes);
+  }
+
+  // kernel arguments of the two launches (pass 1, pass 2) over `ranks`; advances the
+  // workers' counter bases.  Algorithmic bytes per task: A + B + X + G.
+  LsqbBatch build_lsqb_batch(const std::vector<int64_t>& ranks, double* bytes_out) {
+    LsqbBatch b{};
+    b.ntasks = int(ranks.size());
+    b.err = err_dev_;
+    b.spin_ticks = spin_ticks();
+    int blocks1 = 0, blocks2 = 0;
+    double bytes = 0;
+    const int per1 = std::max(1, kLsqbGrid1 / b.ntasks), per2 = std::max(1, kLsqbGrid2 / b.ntasks);
+    for (int k = 0; k < b.ntasks; ++k) {
+      const int64_t rank = ranks[size_t(k)];
+      HipWorker& w = w_[size_t(rank - 1)];
+      const TaskSpec& ts = tasks_[size_t(rank - 1)];
+      LsqbTask& t = b.t[k];
+      t.A = ts.A;
+      t.B = ts.b;
+      t.X = w.x;
+      t.out = w.out;
+      t.R = w.lsqb_R;
+      t.slab = w.lsqb_slab;
+      t.ctr = w.lsqb_ctr;
+      t.flag = w.flag_dev;
+      t.seq = w.seq;
+      t.rows = ts.rows;
+      t.lda = ts.lda;
+      t.cols = int(ts.cols);
+      const int64_t nblocks = (ts.rows + 255) / 256;
+      t.grid1 = int(std::max<int64_t>(1, std::min<int64_t>(nblocks, per1)));
+      t.nslice = int((ts.cols + 255) / 256);
+      const int64_t ksteps = (ts.rows + 31) / 32;
+      int64_t nr = per2 / t.nslice;
+      if (nr >= 8) nr -= nr % 8;  // equal blk % 8 for the slices of a range (one XCD's L2)
+      nr = std::max<int64_t>(1, std::min<int64_t>({nr, int64_t(kLsqbRangeCap), std::max<int64_t>(ksteps, 1)}));
+      t.nrange = int(nr);
+      t.sbase = w.lsqb_sbase;
+      t.tbase = w.lsqb_tbase;
+      w.lsqb_sbase += uint32_t(t.nrange);
+      w.lsqb_tbase += uint32_t(t.nslice);
+      b.block1[k] = blocks1;
+      b.block2[k] = blocks2;
+      blocks1 += t.grid1;
+      blocks2 += t.nrange * t.nslice;
+      bytes += 2.0 * double(ts.rows) * double(ts.cols) + 2.0 * double(ts.rows) * double(ts.k) +
+               2.0 * double(ts.cols) * double(ts.k) + 4.0 * double(ts.cols) * double(ts.k);
+    }
+    b.block1[b.ntasks] = blocks1;
+    b.block2[b.ntasks] = blocks2;
+    *bytes_out = bytes;
+    return b;
+  }
+
+  void enqueue_lsqb(const LsqbBatch& b, hipStream_t s, double bytes) {
+    TimedLaunch tl{};
+    const bool timed = timing_;
+    if (timed) {
+      std::lock_guard<std::mutex> lk(tm_mu_);
+      tl.start = take_event();
+      tl.stop = take_event();
+      tl.bytes = bytes;
+      HIPCHECK(hipEventRecord(tl.start, s));
+    }
+    HIPCHECK(launch_lsqb(b, s));
+    if (timed) {
+      HIPCHECK(hipEventRecord(tl.stop, s));
+      std::lock_guard<std::mutex> lk(tm_mu_);
+      timed_.push_back(tl);
+    }
   }
 
   // enqueue one least-squares launch on `s` (coordinator / server thread or timer thread)

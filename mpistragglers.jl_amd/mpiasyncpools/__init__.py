@@ -5,9 +5,9 @@ completion words.  See DESIGN.md at the repository root.
 from ._capi import lib  # noqa: F401  (fails loudly if the HIP library is not built)
 from .comm import DeviceComm, DistComm, SimComm, generate  # noqa: F401
 from .pool import (ArgumentError, DeviceError, DimensionMismatch, ErrorException,  # noqa: F401
-                   MPIAsyncPool, asyncmap, asyncmap_, lsq_descent, waitall, waitall_)
+                   MPIAsyncPool, asyncmap, asyncmap_, first_plus, lsq_descent, lsqb_descent, waitall, waitall_)
 
 lib()
 
-__all__ = ["MPIAsyncPool", "asyncmap_", "waitall_", "asyncmap", "waitall", "lsq_descent", "DeviceComm", "DistComm",
+__all__ = ["MPIAsyncPool", "asyncmap_", "waitall_", "asyncmap", "waitall", "lsq_descent", "lsqb_descent", "first_plus", "DeviceComm", "DistComm",
            "SimComm", "generate", "ArgumentError", "DimensionMismatch", "ErrorException", "DeviceError"]

@@ -49,6 +49,7 @@ SIGNATURES = [
     ("mpa_comm_set_stream", C.c_int, [_vp, _vp]),
     ("mpa_comm_set_task_kmap", C.c_int, [_vp, C.c_int64, C.c_int]),
     ("mpa_comm_set_task_lsq", C.c_int, [_vp, C.c_int64, C.c_int, C.c_int64, C.c_int64, _vp, C.c_int64, _vp]),
+    ("mpa_comm_set_task_lsq_batch", C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, _vp, C.c_int64, _vp]),
     ("mpa_comm_set_delays", C.c_int, [_vp, C.c_int64, _vp, C.c_int64]),
     ("mpa_comm_tasks_done", C.c_int64, [_vp, C.c_int64]),
     ("mpa_comm_shutdown", C.c_int, [_vp]),
@@ -64,6 +65,10 @@ SIGNATURES = [
     ("mpa_lsq_update", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int64, C.c_int64, _vp, C.c_double]),
     ("mpa_lsq_descent", C.c_int, [_vp, _vp, C.c_int, _vp, C.c_int64, _vp, _vp, _vp, C.c_int, C.c_int64, _vp, _vp,
                                   C.c_double, C.c_double, C.c_int64]),
+    ("mpa_nwait_first_plus", C.c_int, [_vp, C.c_int64, _vp, C.c_int64]),
+    ("mpa_lsqb_update", C.c_int, [_vp, _vp, _vp, _vp, C.c_int64, C.c_int64, _vp, C.c_double]),
+    ("mpa_lsqb_descent", C.c_int, [_vp, _vp, _vp, _vp, C.c_int64, _vp, _vp, _vp, C.c_int, C.c_int64, _vp, _vp,
+                                   C.c_double, C.c_double, C.c_int64]),
     ("mpa_generate", C.c_int, [_vp, C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_int64, C.c_double, _vp]),
 ]
 

@@ -8,6 +8,7 @@ worker runs a registered task kernel on its own HIP stream:
     comm = DeviceComm(n)                      # HIP transport, current GPU
     comm.set_task(rank, "kmap2")              # the reference's test worker programs
     comm.set_task_lsq(rank, A_i, b_i)         # g_i = A_i^T (A_i x - b_i)
+    comm.set_task_lsq_batch(rank, A_i, B_i)   # G_i = A_i^T (A_i X - B_i), 64 iterates (bf16)
     comm.set_delays(rank, delays_ns)          # straggler emulation
 
 `SimComm` is a deterministic virtual-clock host transport used only to test the pool
@@ -118,6 +119,23 @@ class DeviceComm(_Comm):
                                           C.c_void_p(A.data_ptr()), lda, C.c_void_p(b.data_ptr())))
         self._keep[int(rank)] = (A, b)
 
+    def set_task_lsq_batch(self, rank, A, B, cols=None, lda=None):
+        """G = A^T (A X - B): the batched 64-iterate variant (bf16 in, fp32 G).
+
+        A (rows x lda, bf16, row-major), B (rows x 64, bf16) on the GPU; the message X is
+        cols x 64 bf16 and the reply G is cols x 64 fp32 (both row-major)."""
+        import torch
+        if A.dim() != 2 or B.dim() != 2 or A.shape[0] != B.shape[0]:
+            raise ArgumentError("A must be rows x lda and B rows x k")
+        if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16:
+            raise ArgumentError("the batched variant takes bf16 A and B")
+        rows, ld = A.shape
+        cols = ld if cols is None else int(cols)
+        lda = ld if lda is None else int(lda)
+        check(lib().mpa_comm_set_task_lsq_batch(self._h, int(rank), int(rows), cols, int(B.shape[1]),
+                                                C.c_void_p(A.data_ptr()), lda, C.c_void_p(B.data_ptr())))
+        self._keep[int(rank)] = (A, B)
+
     def set_timing(self, enable):
         """Time every least-squares launch with HIP events on its own stream."""
         check(lib().mpa_comm_set_timing(self._h, 1 if enable else 0))
@@ -143,6 +161,14 @@ class DeviceComm(_Comm):
         check(lib().mpa_lsq_update(self._h, dtype_code(x), C.c_void_p(x.data_ptr()),
                                    C.c_void_p(recvbuf.data_ptr()), int(nchunks), int(x.numel()),
                                    w.ctypes.data, float(eta)))
+
+    def lsqb_update(self, x32, xb16, recvbuf, nchunks, weights, eta):
+        """Batched variant: x32 -= eta * sum_i weights[i] * G_i ; xb16 = bf16(x32) (one kernel)."""
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        self._before_call(x32)
+        check(lib().mpa_lsqb_update(self._h, C.c_void_p(x32.data_ptr()), C.c_void_p(xb16.data_ptr()),
+                                    C.c_void_p(recvbuf.data_ptr()), int(nchunks), int(x32.numel()),
+                                    w.ctypes.data, float(eta)))
 
 
 class DistComm(DeviceComm):

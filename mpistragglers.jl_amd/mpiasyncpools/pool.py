@@ -191,13 +191,45 @@ def lsq_descent(pool, comm, x, recvbuf, isendbuf, irecvbuf, nwait, eta, epochs, 
     (mpa_lsq_descent): asyncmap_(...; nwait) then x -= eta * n/sum(w) * sum_i w_i g_i with
     w_i = 1 for fresh chunks, stale_weight for older ones."""
     from .comm import dtype_code
-    if not isinstance(nwait, (int, np.integer)) or isinstance(nwait, bool):
-        raise ArgumentError("lsq_descent takes an integer nwait")
+    kind, k, fn, ctx = _native_nwait(nwait)
     comm._before_call(x)
     check(lib().mpa_lsq_descent(pool._h, comm._h, dtype_code(x), C.c_void_p(x.data_ptr()), int(x.numel()),
                                 C.c_void_p(recvbuf.data_ptr()), C.c_void_p(isendbuf.data_ptr()),
-                                C.c_void_p(irecvbuf.data_ptr()), _capi.MPA_NWAIT_INT, int(nwait), None, None,
+                                C.c_void_p(irecvbuf.data_ptr()), kind, k, fn, ctx,
                                 float(eta), float(stale_weight), int(epochs)))
+    return pool.repochs
+
+
+def first_plus(k):
+    """nwait for the native loops: worker 1 fresh and >= k of the others fresh
+    (mpa_nwait_first_plus; the predicate of test/kmap2.jl:65 widened to k-of-n)."""
+    return ("first_plus", int(k))
+
+
+_CTX_KEEP = []
+
+
+def _native_nwait(nwait):
+    """(kind, int nwait, fn pointer, ctx) for the native descent loops."""
+    if isinstance(nwait, tuple) and len(nwait) == 2 and nwait[0] == "first_plus":
+        ctx = C.c_int64(nwait[1])
+        _CTX_KEEP.append(ctx)
+        fn = C.cast(lib().mpa_nwait_first_plus, C.c_void_p)
+        return _capi.MPA_NWAIT_FN, 0, fn, C.cast(C.byref(ctx), C.c_void_p)
+    if not isinstance(nwait, (int, np.integer)) or isinstance(nwait, bool):
+        raise ArgumentError("the native loops take an integer nwait or first_plus(k)")
+    return _capi.MPA_NWAIT_INT, int(nwait), None, None
+
+
+def lsqb_descent(pool, comm, x32, xb16, recvbuf, isendbuf, irecvbuf, nwait, eta, epochs, stale_weight=0.0):
+    """mpa_lsqb_descent: the coordinator loop of the batched 64-iterate variant.  x32 is the
+    fp32 master iterate (cols x 64), xb16 its bf16 rounding = the message."""
+    kind, k, fn, ctx = _native_nwait(nwait)
+    comm._before_call(x32)
+    check(lib().mpa_lsqb_descent(pool._h, comm._h, C.c_void_p(x32.data_ptr()), C.c_void_p(xb16.data_ptr()),
+                                 int(x32.numel()), C.c_void_p(recvbuf.data_ptr()), C.c_void_p(isendbuf.data_ptr()),
+                                 C.c_void_p(irecvbuf.data_ptr()), kind, k, fn, ctx,
+                                 float(eta), float(stale_weight), int(epochs)))
     return pool.repochs
 
 

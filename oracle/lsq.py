@@ -116,7 +116,7 @@ def shard_gradient(A, b, x, dtype="f32"):
 def batched_shard_gradient(A, B, X, dtype="bf16"):
     """G = A^T (A X - B) for the 64-iterate variant; X is cols x k, B is rows x k."""
     A64 = as_f64(A, dtype)
-    R = A64 @ as_f64(X, dtype) - np.asarray(B, dtype=np.float64)
+    R = A64 @ as_f64(X, dtype) - as_f64(B, dtype)
     return A64.T @ R
 
 
