@@ -37,7 +37,19 @@ def _problem(rows, cols, seed):
     return A, B, X
 
 
-def _run(M, torch, shards, cols, X, nwait=None, comm=None, pool=None, delays=None):
+class _Bufs:
+    """sendbuf / recvbuf / isendbuf / irecvbuf, allocated once: the reference requires the
+    same isendbuf / irecvbuf on every call (in-flight requests point at them,
+    src/MPIAsyncPools.jl:63-66)."""
+
+    def __init__(self, torch, n, cols):
+        self.send = torch.zeros(cols * K, dtype=torch.bfloat16, device="cuda")
+        self.isend = torch.zeros(n * cols * K, dtype=torch.bfloat16, device="cuda")
+        self.recv = torch.zeros(n * cols * K, dtype=torch.float32, device="cuda")
+        self.irecv = torch.zeros_like(self.recv)
+
+
+def _run(M, torch, shards, cols, X, nwait=None, comm=None, pool=None, delays=None, bufs=None):
     n = len(shards)
     if comm is None:
         comm = M.DeviceComm(n)
@@ -46,12 +58,11 @@ def _run(M, torch, shards, cols, X, nwait=None, comm=None, pool=None, delays=Non
             if delays is not None:
                 comm.set_delays(r, delays[r - 1])
         pool = M.MPIAsyncPool(n)
-    send = _bf16(torch, X)
-    isend = torch.zeros(n * cols * K, dtype=torch.bfloat16, device="cuda")
-    recv = torch.zeros(n * cols * K, dtype=torch.float32, device="cuda")
-    irecv = torch.zeros_like(recv)
-    rep = M.asyncmap_(pool, send, recv, isend, irecv, comm, nwait=n if nwait is None else nwait)
-    return recv.cpu().numpy().reshape(n, cols, K), rep, comm, pool
+    if bufs is None:
+        bufs = comm._bufs = _Bufs(torch, n, cols)
+    bufs.send.copy_(_bf16(torch, X).view(-1))
+    rep = M.asyncmap_(pool, bufs.send, bufs.recv, bufs.isend, bufs.irecv, comm, nwait=n if nwait is None else nwait)
+    return bufs.recv.cpu().numpy().reshape(n, cols, K), rep, comm, pool
 
 
 @pytest.mark.parametrize("rows,cols", [(1, 32), (100, 64), (1000, 256), (4113, 544), (3000, 2048), (257, 4096),
@@ -85,7 +96,7 @@ def test_lsqb_batched_launch_counters_and_determinism(M):
     for i in range(3):
         assert lsq.rel_err(out[i], refs[i]) <= TOL, i
     for _ in range(3):
-        again, rep, _, _ = _run(M, torch, shards, cols, X, comm=comm, pool=pool)
+        again, rep, _, _ = _run(M, torch, shards, cols, X, comm=comm, pool=pool, bufs=comm._bufs)
         assert np.array_equal(again.view(np.uint32), out.view(np.uint32))
     comm.close()
 
@@ -106,7 +117,8 @@ def test_lsqb_stragglers_chunks_match_their_epochs(M):
         X = lsq.gen_matrix(100 + epoch, 0, cols, K, "bf16", stream=lsq.STREAM_X, scale=np.float32(0.5))
         sent[epoch] = X
         out, rep, comm, pool = _run(M, torch, shards, cols, X, nwait=1, comm=comm, pool=pool,
-                                    delays=delays if comm is None else None)
+                                    delays=delays if comm is None else None,
+                                    bufs=None if comm is None else comm._bufs)
         assert (rep == epoch).sum() >= 1
         for i in range(n):
             if rep[i] == 0:
