@@ -25,6 +25,9 @@ struct CallBufs {
   uint8_t* irecvbuf = nullptr;
   size_t rl = 0;  // bytes per recv chunk (:81)
   int64_t n = 0;  // pool size
+  // the call returns only once every task it posts has completed (integer nwait == n), so
+  // a transport may order those tasks on the coordinator's own stream
+  bool await_all = false;
 };
 
 struct TaskSpec {

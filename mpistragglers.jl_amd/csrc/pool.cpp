@@ -75,6 +75,7 @@ void asyncmap(Pool& p, const AsyncmapArgs& a) {
   b.irecvbuf = static_cast<uint8_t*>(a.irecvbuf);
   b.rl = a.irecv_bytes / size_t(comm_size);
   b.n = comm_size;
+  b.await_all = a.nwait_kind == MPA_NWAIT_INT && a.nwait == comm_size;
   c.begin_call(b);
 
   p.epoch = a.epoch;                                                               // :87

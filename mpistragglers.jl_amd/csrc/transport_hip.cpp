@@ -73,7 +73,19 @@ constexpr int kLsqbRangeCap = 128;
 std::mutex g_stream_mu;
 std::vector<std::pair<int, hipStream_t>> g_free_streams;
 
+// The pooled streams (and their HSA queues) are destroyed at process exit, before the HIP
+// runtime's own teardown (atexit handlers run in reverse registration order, and the runtime
+// registers its teardown when it is loaded, before the first stream here): a profiler that
+// tears down while queues are still alive crashed in __cxa_finalize.
+void destroy_pooled_streams() {
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  for (auto& ds : g_free_streams) (void)hipStreamDestroy(ds.second);
+  g_free_streams.clear();
+}
+
 hipStream_t make_queue_stream(int device) {
+  static const bool registered = (std::atexit(destroy_pooled_streams), true);
+  (void)registered;
   {
     std::lock_guard<std::mutex> lk(g_stream_mu);
     for (size_t k = 0; k < g_free_streams.size(); ++k)
@@ -367,11 +379,13 @@ class HipComm final : public Comm {
     xb.launch();
     harv_.clear();
     if (local_posts) {
-      HIPCHECK(hipEventRecord(xfer_ev_, coord_));
       std::vector<int64_t> here;
       for (int64_t rank : posts_)
         if (!w_[size_t(rank - 1)].remote) here.push_back(rank);
-      launch_tasks(here, /*staged=*/false);
+      // every task of this call is awaited before the caller enqueues anything else on the
+      // coordinator stream: run the batch right behind the exchange on that stream (a
+      // cross-queue event wait costs ~35 us per epoch, profiles/r01_c2_gaps.json)
+      launch_tasks(here, /*staged=*/false, /*on_coord=*/b_.await_all);
     }
     posts_.clear();
   }
@@ -603,15 +617,24 @@ class HipComm final : public Comm {
   // own stream behind a delay kernel, so a straggler never holds back another worker;
   // reference-test tasks (kmap/echo) run per worker.  `staged`: the message sits in a
   // mailbox and is first copied into the worker's device slot on the launch's stream.
-  void launch_tasks(const std::vector<int64_t>& ranks, bool staged) {
+  void launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool on_coord = false) {
     std::vector<int64_t> batch;
     int batch_kind = -1, batch_dtype = -1, batch_cp = 0;
     hipStream_t bs = nullptr;
+    bool ev_recorded = false;
+    // the exchange that delivered the messages, as an event for other streams (once)
+    auto after_exchange = [&](hipStream_t s) {
+      if (!ev_recorded) {
+        HIPCHECK(hipEventRecord(xfer_ev_, coord_));
+        ev_recorded = true;
+      }
+      HIPCHECK(hipStreamWaitEvent(s, xfer_ev_, 0));
+    };
     auto emit = [&]() {
       if (batch.empty()) return;
-      bs = pick_launch_stream();
+      bs = on_coord && !staged ? coord_ : pick_launch_stream();
       if (staged) stage_in(batch, bs);
-      else HIPCHECK(hipStreamWaitEvent(bs, xfer_ev_, 0));
+      else if (bs != coord_) after_exchange(bs);
       if (batch_kind == MPA_TASK_LSQ_BATCH) launch_lsqb_batch(batch, bs);
       else launch_lsq_batch(batch, batch_dtype, bs);
       batch.clear();
@@ -635,7 +658,7 @@ class HipComm final : public Comm {
       // The message is delivered now (stream-ordered after the exchange / stage-in); a
       // delayed worker "sleeps" on the host timer and only then computes.
       if (staged) stage_in({rank}, w.stream);
-      else HIPCHECK(hipStreamWaitEvent(w.stream, xfer_ev_, 0));
+      else after_exchange(w.stream);
       std::function<void()> go;
       if (ts.kind == MPA_TASK_LSQ) {
         double bytes = 0;
