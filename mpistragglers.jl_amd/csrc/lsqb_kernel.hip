@@ -78,14 +78,17 @@ __device__ __forceinline__ int task_of(const int* block0, int ntasks) {
 }
 
 // ---------------------------------------------------------------------------------------
-// pass 1: R = A X - B.  Workgroup = 4 waves x 64 rows; X streams through LDS in chunks of
-// 128 rows (double buffered, shared by the 4 waves), A goes straight to registers as the
-// MFMA A operand (each lane 16 B; the four lanes of a row read 64 contiguous bytes).
-constexpr int P1_KC = 128;          // X rows per LDS chunk
+// pass 1: R = A X - B.  Workgroup = 8 waves x 32 rows (2 MFMA row tiles per wave); X
+// streams through LDS in chunks of 128 rows (double buffered, shared by the 8 waves); A
+// goes straight to registers as the MFMA A operand (each lane 16 B; the four lanes of a
+// row read 64 contiguous bytes), prefetched one whole chunk (4 k-steps, 8 KiB per wave)
+// ahead so every CU keeps >= 64 KiB of HBM reads in flight (MI355X_MICROARCH.md §HBM).
+constexpr int P1_THREADS = 512;
+constexpr int P1_KC = 128;          // X rows per LDS chunk = 4 k-steps of 32
 constexpr int P1_XS = K * 2 + 16;   // LDS bytes per X row (pad: 2-way tr reads at most)
-constexpr int P1_WG_ROWS = 256;
+constexpr int P1_WG_ROWS = 256;     // 8 waves x 32 rows
 
-__global__ void __launch_bounds__(kThreads) lsqb_resid_kernel(LsqbBatch batch) {
+__global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch) {
   __shared__ __attribute__((aligned(16))) uint8_t xs[2][P1_KC * P1_XS];
   const int ti = task_of(batch.block1, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
@@ -97,73 +100,56 @@ __global__ void __launch_bounds__(kThreads) lsqb_resid_kernel(LsqbBatch batch) {
   const int nblocks = int((rows + P1_WG_ROWS - 1) / P1_WG_ROWS);
   if (blk >= nblocks) return;  // whole workgroup
   const int nchunk = (cols + P1_KC - 1) / P1_KC;
+  const int grid1 = a.grid1;
   const uint16_t* __restrict__ A = static_cast<const uint16_t*>(a.A);
   const uint16_t* __restrict__ Bm = static_cast<const uint16_t*>(a.B);
   const uint8_t* __restrict__ X = static_cast<const uint8_t*>(a.X);
   uint8_t* __restrict__ R = static_cast<uint8_t*>(a.R);
 
-  // X chunk c: rows [c*KC, c*KC + KC); thread t moves 16-B piece (t&7) of rows (t>>3) + 32q
-  uint4 xr[4];
+  // X chunk c: rows [c*KC, c*KC + KC); thread t moves 16-B piece (t&7) of rows (t>>3) + 64q
+  uint4 xr[2];
   auto load_x = [&](int c) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = c * P1_KC + (tid >> 3) + 32 * q;
+    for (int q = 0; q < 2; ++q) {
+      const int r = c * P1_KC + (tid >> 3) + 64 * q;
       xr[q] = r < cols ? ld16(X + size_t(r) * (K * 2) + (tid & 7) * 16) : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_x = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<uint4*>(&xs[buf][((tid >> 3) + 32 * q) * P1_XS + (tid & 7) * 16]) = xr[q];
+    for (int q = 0; q < 2; ++q)
+      *reinterpret_cast<uint4*>(&xs[buf][((tid >> 3) + 64 * q) * P1_XS + (tid & 7) * 16]) = xr[q];
+  };
+  // A operand fragments of chunk c of row block rbx: F[k-step][row tile]
+  typedef bf16x8 Frags[4][2];
+  auto load_a = [&](Frags& F, int rbx, int c) {
+    const uint16_t* p[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      int64_t r = int64_t(rbx) * P1_WG_ROWS + wave * 32 + 16 * m + i;
+      r = r < rows ? r : rows - 1;
+      p[m] = A + r * a.lda + 8 * g + c * P1_KC;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (c * P1_KC + 32 * s < cols)  // wave-uniform (cols % 32 == 0)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) F[s][m] = __builtin_bit_cast(bf16x8, ld16_nt(p[m] + 32 * s));
   };
 
-  load_x(0);
-  store_x(0);
-  __syncthreads();
-  int cur = 0;
-  for (int rb = blk; rb < nblocks; rb += a.grid1) {
-    const int64_t row_w = int64_t(rb) * P1_WG_ROWS + wave * 64;
-    const uint16_t* arow[4];
+  f32x4 acc[2][4];
+  auto zero_acc = [&]() {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      int64_t r = row_w + 16 * m + i;
-      r = r < rows ? r : rows - 1;
-      arow[m] = A + r * a.lda + 8 * g;
-    }
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int c = 0; c < nchunk; ++c) {
-      const bool last_chunk = c + 1 == nchunk;
-      const bool more = !(last_chunk && rb + a.grid1 >= nblocks);
-      if (more) load_x(last_chunk ? 0 : c + 1);
-      const uint8_t* tile = xs[cur];
+  };
+  // R = acc - B, split hi/lo, into the k-packed layout: entry (row/8, iterate) = 32 B =
+  // hi[8] | lo[8] (element row%8).  This lane holds rows row_w+16m+4g+r, iterate 16t+i.
+  auto epilogue = [&](int rbx) {
+    const int64_t row_w = int64_t(rbx) * P1_WG_ROWS + wave * 32;
 #pragma unroll
-      for (int s = 0; s < P1_KC / 32; ++s) {
-        const int k0 = c * P1_KC + 32 * s;
-        if (k0 >= cols) break;  // wave-uniform (cols % 32 == 0)
-        bf16x8 af[4], bf[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) af[m] = __builtin_bit_cast(bf16x8, ld16_nt(arow[m] + k0));
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bf[t] = tr_operand(tile, P1_XS, 32 * s, 32 * t, lane);
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int t = 0; t < 4; ++t) acc[m][t] = mfma(af[m], bf[t], acc[m][t]);
-      }
-      if (more) store_x(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
-    }
-
-    // R = acc - B, split hi/lo, into the k-packed layout: entry (row/8, iterate) = 32 B =
-    // hi[8] | lo[8] (element row%8).  This lane holds rows row_w+16m+4g+r, iterate 16t+i.
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < 2; ++m) {
       const int64_t r0 = row_w + 16 * m + 4 * g;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -184,6 +170,52 @@ __global__ void __launch_bounds__(kThreads) lsqb_resid_kernel(LsqbBatch batch) {
                                                        uint32_t(lo[2]) | (uint32_t(lo[3]) << 16));
       }
     }
+  };
+
+  int rb = blk, c = 0, cur = 0;
+  Frags FA, FB;
+  load_x(0);
+  load_a(FA, rb, 0);
+  store_x(0);
+  zero_acc();
+  __syncthreads();
+  // one chunk: prefetch the next chunk's A fragments and X rows, compute this chunk from
+  // registers + LDS, publish the next X chunk, and finish the row block after its last chunk
+  auto step = [&](Frags& F, Frags& N) -> bool {
+    int rbn = rb, cn = c + 1;
+    if (cn == nchunk) {
+      cn = 0;
+      rbn = rb + grid1;
+    }
+    const bool more = rbn < nblocks;
+    if (more) {
+      load_a(N, rbn, cn);
+      load_x(cn);
+    }
+    const uint8_t* tile = xs[cur];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (c * P1_KC + 32 * s >= cols) break;  // wave-uniform
+      bf16x8 bf[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bf[t] = tr_operand(tile, P1_XS, 32 * s, 32 * t, lane);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[m][t] = mfma(F[s][m], bf[t], acc[m][t]);
+    }
+    if (more) store_x(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+    if (rbn != rb) {
+      epilogue(rb);
+      zero_acc();
+    }
+    rb = rbn;
+    c = cn;
+    return more;
+  };
+  while (step(FA, FB) && step(FB, FA)) {
   }
 }
 
@@ -191,8 +223,9 @@ __global__ void __launch_bounds__(kThreads) lsqb_resid_kernel(LsqbBatch batch) {
 // pass 2: G = A^T R.  Workgroup (range rho, slice sigma): rows [32*s_begin, 32*s_end) x
 // columns [256 sigma, 256 sigma + 256); wave w owns columns 64w..64w+63 of the slice and all
 // 64 iterates (acc 4 x 4 tiles: G^T[iterate][column]).  Per k-step (32 rows) the A tile
-// (32 x 256 bf16 = 16 KiB) is staged in LDS (double buffered, loaded one step ahead) and
-// read transposed as the B operand; R_hi / R_lo fragments are one 16-B load each.
+// (32 x 256 bf16 = 16 KiB) is staged in LDS (double buffered) and read transposed as the B
+// operand; R_hi / R_lo fragments are one 16-B load each.  Software pipeline: the tile of
+// step s+2 and the R fragments of step s+1 are in flight while step s computes.
 constexpr int P2_CW = 256;
 constexpr int P2_AS = P2_CW * 2 + 16;
 constexpr int P2_PART = K * P2_CW;  // floats per workgroup partial
@@ -218,19 +251,28 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
   // tile loader: thread t moves 16 B (8 columns) = chunk (t&31) of rows (t>>5) + 8q
   const int lc = c0 + 8 * (tid & 31);
   const bool lc_ok = lc < cols;
-  uint4 tr_[4];
-  auto load_tile = [&](int64_t s) {
+  typedef uint4 Tile[4];
+  typedef bf16x8 RFr[2][4];  // [hi, lo][iterate tile]
+  auto load_tile = [&](Tile& T, int64_t s) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       int64_t r = 32 * s + (tid >> 5) + 8 * q;
       r = r < rows ? r : rows - 1;  // rows past the end meet R = 0 (pass 1 zero-fills)
-      tr_[q] = lc_ok ? ld16_nt(A + r * a.lda + lc) : make_uint4(0, 0, 0, 0);
+      T[q] = lc_ok ? ld16_nt(A + r * a.lda + lc) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](const Tile& T, int buf) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<uint4*>(&as_[buf][((tid >> 5) + 8 * q) * P2_AS + 16 * (tid & 31)]) = tr_[q];
+      *reinterpret_cast<uint4*>(&as_[buf][((tid >> 5) + 8 * q) * P2_AS + 16 * (tid & 31)]) = T[q];
+  };
+  auto load_r = [&](RFr& F, int64_t s) {
+    const uint8_t* re = R + ((size_t(4 * s + g) * K + i) * 32);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      F[0][u] = __builtin_bit_cast(bf16x8, ld16(re + size_t(16 * u) * 32));
+      F[1][u] = __builtin_bit_cast(bf16x8, ld16(re + size_t(16 * u) * 32 + 16));
+    }
   };
 
   f32x4 acc[4][4];
@@ -239,34 +281,39 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (s_begin < s_end) {
-    load_tile(s_begin);
-    store_tile(0);
+  Tile TA, TB;
+  RFr RA, RB;
+  int64_t s = s_begin;
+  if (s < s_end) {
+    load_tile(TA, s);
+    if (s + 1 < s_end) load_tile(TB, s + 1);
+    load_r(RA, s);
+    store_tile(TA, 0);
   }
   __syncthreads();
   int cur = 0;
-  for (int64_t s = s_begin; s < s_end; ++s) {
-    const bool more = s + 1 < s_end;
-    if (more) load_tile(s + 1);
-    bf16x8 rh[4], rl[4], bf[4];
-    const uint8_t* re = R + ((size_t(4 * s + g) * K + i) * 32);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      rh[u] = __builtin_bit_cast(bf16x8, ld16(re + size_t(16 * u) * 32));
-      rl[u] = __builtin_bit_cast(bf16x8, ld16(re + size_t(16 * u) * 32 + 16));
-    }
+  // step s: LDS buf[cur] holds tile s, Tn holds tile s+1 (in flight), Rc the R fragments of s
+  auto step = [&](Tile& Tf, Tile& Tn, RFr& Rc, RFr& Rn) -> bool {
+    if (s >= s_end) return false;
+    if (s + 2 < s_end) load_tile(Tf, s + 2);
+    if (s + 1 < s_end) load_r(Rn, s + 1);
+    bf16x8 bf[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) bf[t] = tr_operand(as_[cur], P2_AS, 0, 2 * (64 * wave + 16 * t), lane);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        acc[u][t] = mfma(rh[u], bf[t], acc[u][t]);
-        acc[u][t] = mfma(rl[u], bf[t], acc[u][t]);
+        acc[u][t] = mfma(Rc[0][u], bf[t], acc[u][t]);
+        acc[u][t] = mfma(Rc[1][u], bf[t], acc[u][t]);
       }
-    if (more) store_tile(cur ^ 1);
+    if (s + 1 < s_end) store_tile(Tn, cur ^ 1);
     __syncthreads();
     cur ^= 1;
+    ++s;
+    return true;
+  };
+  while (step(TA, TB, RA, RB) && step(TB, TA, RB, RA)) {
   }
 
   // partial of this workgroup: slab[(rho * nslice + sigma)][wave][u][t][lane][4]
@@ -327,7 +374,7 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
 hipError_t launch_lsqb(const LsqbBatch& a, hipStream_t s) {
   const int g1 = a.block1[a.ntasks], g2 = a.block2[a.ntasks];
   if (g1 <= 0 || g2 <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lsqb_resid_kernel, dim3(g1), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(lsqb_resid_kernel, dim3(g1), dim3(P1_THREADS), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(lsqb_grad_kernel, dim3(g2), dim3(kThreads), 0, s, a);

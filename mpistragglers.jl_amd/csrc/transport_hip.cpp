@@ -60,10 +60,10 @@ using Clock = std::chrono::steady_clock;
 constexpr int kDefaultLaunchGrid = 512;  // 2 workgroups per CU: profiles/r01_tune_sweep2.jsonl
 constexpr int kSlabGridCap = 1024;       // most workgroups a single task may be given
 constexpr int kLaunchStreams = 2;
-// batched multi-iterate task: pass-1 / pass-2 workgroups per launch (resident: 2 / 4 per
-// CU by VGPRs), and the most row ranges a pass-2 task is split into
-constexpr int kLsqbGrid1 = 512;
-constexpr int kLsqbGrid2 = 1024;
+// batched multi-iterate task: pass-1 / pass-2 workgroups per launch (= resident: 1 x 512 /
+// 2 x 256 threads per CU by VGPRs), and the most row ranges a pass-2 task is split into
+constexpr int kLsqbGrid1 = 256;
+constexpr int kLsqbGrid2 = 512;
 constexpr int kLsqbRangeCap = 128;
 
 // Process-wide pool of CU-masked streams: communicators come and go (tests create many),
