@@ -80,6 +80,8 @@ int lsq_rows_per_wave_iter(int dtype, int cols);
 // B rows x 64 bf16, G cols x 64 fp32 (the reply, row-major).
 constexpr int kLsqbIterates = 64;
 constexpr int kLsqbMaxSlices = 16;  // 256-column slices: cols <= 4096
+constexpr int kLsqbSplitKCols = 2048;  // pass 1 holds X in registers up to this many columns
+constexpr int kLsqbSplitKRows = 16;    // rows per split-K pass-1 block
 struct LsqbTask {
   const void* A;
   const void* B;
@@ -98,6 +100,7 @@ struct LsqbTask {
 };
 struct LsqbBatch {
   int ntasks;
+  int splitk;  // pass 1 = the whole-row split-K kernel (every task cols <= kLsqbSplitKCols)
   unsigned* err;
   unsigned long long spin_ticks;
   int block1[kMaxLsqTasks + 1];

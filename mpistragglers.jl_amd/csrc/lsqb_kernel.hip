@@ -88,7 +88,7 @@ constexpr int P1_KC = 128;          // X rows per LDS chunk = 4 k-steps of 32
 constexpr int P1_XS = K * 2 + 16;   // LDS bytes per X row (pad: 2-way tr reads at most)
 constexpr int P1_WG_ROWS = 256;     // 8 waves x 32 rows
 
-__global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch) {
+__global__ void __launch_bounds__(P1_THREADS) lsqb_resid_chunked_kernel(LsqbBatch batch) {
   __shared__ __attribute__((aligned(16))) uint8_t xs[2][P1_KC * P1_XS];
   const int ti = task_of(batch.block1, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
@@ -213,6 +213,125 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
     }
     rb = rbn;
     c = cn;
+    return more;
+  };
+  while (step(FA, FB) && step(FB, FA)) {
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// pass 1, cols <= 2048 (the c5 shape): split K over the 8 waves of the workgroup so the
+// workgroup streams WHOLE rows.  Wave w owns columns [256w, 256w + 256) and holds that
+// slice of X in registers for the whole kernel (8 k-steps x 4 iterate tiles of MFMA B
+// operand = 128 VGPRs, transposed once through LDS); per block of 16 rows it reads
+// A[16 rows][its 256 columns] (the 8 waves together: 16 contiguous rows = 64 KiB), the
+// next block's fragments already in flight, and the 8 partial residuals are summed in LDS
+// in wave order.  The chunked kernel above re-reads X per row block and walks every row in
+// 256-B pieces 4 KiB apart, which left DRAM pages half used (3.3 TB/s, profiles/).
+constexpr int Q_ROWS = 16;
+constexpr int Q_KW = 256;                  // columns per wave
+constexpr int Q_XS = K * 2 + 16;           // LDS bytes per staged X row
+constexpr int Q_STAGE = 32 * Q_XS;         // one wave's staging window (one k-step of X)
+constexpr int Q_PK = K + 4;                // partial-residual row stride (floats; conflict-free)
+constexpr int Q_PART = Q_ROWS * Q_PK * 4;  // one wave's partial residual (fp32)
+
+__global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch) {
+  constexpr int LDS = (8 * Q_STAGE > 8 * Q_PART ? 8 * Q_STAGE : 8 * Q_PART);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+  const int ti = task_of(batch.block1, batch.ntasks);
+  const LsqbTask& a = batch.t[ti];
+  const int blk = int(blockIdx.x) - batch.block1[ti];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t rows = a.rows;
+  const int cols = a.cols;
+  // blocks of 16 rows, an even count: pass 2 reads whole 32-row k-steps, zero past the end
+  const int64_t nblocks = ((rows + 31) / 32) * 2;
+  if (blk >= nblocks) return;  // whole workgroup
+  const int grid1 = a.grid1;
+  const int kc0 = wave * Q_KW;                       // first column of this wave
+  const int nks = cols > kc0 ? ((cols - kc0) < Q_KW ? (cols - kc0) : Q_KW) / 32 : 0;  // its k-steps
+  const uint16_t* __restrict__ A = static_cast<const uint16_t*>(a.A);
+  const uint16_t* __restrict__ Bm = static_cast<const uint16_t*>(a.B);
+  const uint8_t* __restrict__ X = static_cast<const uint8_t*>(a.X);
+  uint8_t* __restrict__ R = static_cast<uint8_t*>(a.R);
+
+  // this wave's X slice as MFMA B operands: XF[k-step][iterate tile]
+  bf16x8 XF[8][4];
+  uint8_t* stage = lds + wave * Q_STAGE;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    if (s < nks) {
+      // 32 X rows (4 KiB) -> the wave's window: lane moves 16-B pieces l, l+64, ..., l+192
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int piece = lane + 64 * q, r = piece >> 3, c16 = piece & 7;
+        *reinterpret_cast<uint4*>(stage + r * Q_XS + c16 * 16) =
+            ld16(X + size_t(kc0 + 32 * s + r) * (K * 2) + c16 * 16);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the window is written (one wave)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) XF[s][t] = tr_operand(stage, Q_XS, 0, 32 * t, lane);
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // reads done before the window is rewritten
+    }
+  }
+  __syncthreads();  // staging windows are reused as the partial-residual buffer below
+
+  typedef bf16x8 Frags[8];
+  auto load_a = [&](Frags& F, int64_t rbx) {
+    int64_t r = rbx * Q_ROWS + i;
+    r = r < rows ? r : rows - 1;
+    const uint16_t* p = A + r * a.lda + kc0 + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s < nks) F[s] = __builtin_bit_cast(bf16x8, ld16_nt(p + 32 * s));
+  };
+  float* part = reinterpret_cast<float*>(lds);  // [wave][16 rows][64 iterates (+4 pad)]
+
+  int64_t rb = blk;
+  Frags FA, FB;
+  load_a(FA, rb);
+  auto step = [&](Frags& F, Frags& N) -> bool {
+    const int64_t rbn = rb + grid1;
+    const bool more = rbn < nblocks;
+    if (more) load_a(N, rbn);
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s < nks)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = mfma(F[s], XF[s][t], acc[t]);
+    // lane holds rows 4g + r, iterate 16t + i of this wave's partial
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[(wave * Q_ROWS + 4 * g + r) * Q_PK + 16 * t + i] = acc[t][r];
+    __syncthreads();
+    // thread -> (row group rg of 8 rows, iterate it, row pair h): sum the 8 waves in order,
+    // subtract B, split hi/lo, store 2 of the 8 rows of R8 entry (row/8, it)
+    {
+      const int it = tid & 63, h = (tid >> 6) & 3, rg = tid >> 8;
+      uint32_t hi2 = 0, lo2 = 0;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int rl = 8 * rg + 2 * h + e;
+        const int64_t row = rb * Q_ROWS + rl;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v += part[(w * Q_ROWS + rl) * Q_PK + it];
+        v = row < rows ? v - bf16_to_f32(Bm[row * K + it]) : 0.f;
+        const uint16_t hv = bf16_rne(v), lv = bf16_rne(v - bf16_to_f32(hv));
+        hi2 |= uint32_t(hv) << (16 * e);
+        lo2 |= uint32_t(lv) << (16 * e);
+      }
+      uint8_t* ent = R + ((size_t((rb * Q_ROWS) / 8 + rg) * K + it) * 32) + 4 * h;
+      *reinterpret_cast<uint32_t*>(ent) = hi2;
+      *reinterpret_cast<uint32_t*>(ent + 16) = lo2;
+    }
+    __syncthreads();
+    rb = rbn;
     return more;
   };
   while (step(FA, FB) && step(FB, FA)) {
@@ -374,7 +493,8 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
 hipError_t launch_lsqb(const LsqbBatch& a, hipStream_t s) {
   const int g1 = a.block1[a.ntasks], g2 = a.block2[a.ntasks];
   if (g1 <= 0 || g2 <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lsqb_resid_kernel, dim3(g1), dim3(P1_THREADS), 0, s, a);
+  if (a.splitk) hipLaunchKernelGGL(lsqb_resid_kernel, dim3(g1), dim3(P1_THREADS), 0, s, a);
+  else hipLaunchKernelGGL(lsqb_resid_chunked_kernel, dim3(g1), dim3(P1_THREADS), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(lsqb_grad_kernel, dim3(g2), dim3(kThreads), 0, s, a);

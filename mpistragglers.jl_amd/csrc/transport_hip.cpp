@@ -893,6 +893,9 @@ class HipComm final : public Comm {
     int blocks1 = 0, blocks2 = 0;
     double bytes = 0;
     const int per1 = std::max(1, kLsqbGrid1 / b.ntasks), per2 = std::max(1, kLsqbGrid2 / b.ntasks);
+    b.splitk = 1;
+    for (int k = 0; k < b.ntasks; ++k)
+      if (tasks_[size_t(ranks[size_t(k)] - 1)].cols > kLsqbSplitKCols) b.splitk = 0;
     for (int k = 0; k < b.ntasks; ++k) {
       const int64_t rank = ranks[size_t(k)];
       HipWorker& w = w_[size_t(rank - 1)];
@@ -910,7 +913,7 @@ class HipComm final : public Comm {
       t.rows = ts.rows;
       t.lda = ts.lda;
       t.cols = int(ts.cols);
-      const int64_t nblocks = (ts.rows + 255) / 256;
+      const int64_t nblocks = b.splitk ? ((ts.rows + 31) / 32) * (32 / kLsqbSplitKRows) : (ts.rows + 255) / 256;
       t.grid1 = int(std::max<int64_t>(1, std::min<int64_t>(nblocks, per1)));
       t.nslice = int((ts.cols + 255) / 256);
       const int64_t ksteps = (ts.rows + 31) / 32;
