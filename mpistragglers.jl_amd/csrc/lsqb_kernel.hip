@@ -288,13 +288,29 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   };
   float* part = reinterpret_cast<float*>(lds);  // [wave][16 rows][64 iterates (+4 pad)]
 
+  // this thread's reduction slot: (row group rg of 8 rows, iterate it, row pair h)
+  const int it = tid & 63, h = (tid >> 6) & 3, rg = tid >> 8;
+  // B of the slot's two rows of block rbx (prefetched with the block's A fragments)
+  auto load_b = [&](uint16_t (&bv)[2], int64_t rbx) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int64_t row = rbx * Q_ROWS + 8 * rg + 2 * h + e;
+      bv[e] = row < rows ? Bm[row * K + it] : uint16_t(0);
+    }
+  };
+
   int64_t rb = blk;
   Frags FA, FB;
+  uint16_t BA[2], BB[2];
   load_a(FA, rb);
-  auto step = [&](Frags& F, Frags& N) -> bool {
+  load_b(BA, rb);
+  auto step = [&](Frags& F, Frags& N, uint16_t (&Bc)[2], uint16_t (&Bn)[2]) -> bool {
     const int64_t rbn = rb + grid1;
     const bool more = rbn < nblocks;
-    if (more) load_a(N, rbn);
+    if (more) {
+      load_a(N, rbn);
+      load_b(Bn, rbn);
+    }
     f32x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -312,7 +328,6 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
     // thread -> (row group rg of 8 rows, iterate it, row pair h): sum the 8 waves in order,
     // subtract B, split hi/lo, store 2 of the 8 rows of R8 entry (row/8, it)
     {
-      const int it = tid & 63, h = (tid >> 6) & 3, rg = tid >> 8;
       uint32_t hi2 = 0, lo2 = 0;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -321,7 +336,7 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
         float v = 0.f;
 #pragma unroll
         for (int w = 0; w < 8; ++w) v += part[(w * Q_ROWS + rl) * Q_PK + it];
-        v = row < rows ? v - bf16_to_f32(Bm[row * K + it]) : 0.f;
+        v = row < rows ? v - bf16_to_f32(Bc[e]) : 0.f;
         const uint16_t hv = bf16_rne(v), lv = bf16_rne(v - bf16_to_f32(hv));
         hi2 |= uint32_t(hv) << (16 * e);
         lo2 |= uint32_t(lv) << (16 * e);
@@ -334,7 +349,7 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
     rb = rbn;
     return more;
   };
-  while (step(FA, FB) && step(FB, FA)) {
+  while (step(FA, FB, BA, BB) && step(FB, FA, BB, BA)) {
   }
 }
 
