@@ -34,5 +34,10 @@ __device__ __forceinline__ void publish_done(unsigned long long* flag, unsigned 
   __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A pre-armed launch whose doorbell was rung with kCancelBit: return before any work.
+__device__ __forceinline__ bool disarmed(const unsigned long long* go) {
+  return go && (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kCancelBit);
+}
+
 }  // namespace dev
 }  // namespace mpa

@@ -24,6 +24,13 @@ using namespace dev;
 
 // ---------------------------------------------------------------------------------------
 __device__ void block_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  if (n == 8 && ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 7u) == 0) {
+    // one word, copied untorn (a doorbell value staged as a pre-armed task's go word)
+    if (threadIdx.x == 0)
+      *reinterpret_cast<unsigned long long*>(dst) =
+          __hip_atomic_load(reinterpret_cast<const unsigned long long*>(src), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15u) == 0) {
     const uint64_t nv = n >> 4;
     uint4* d = reinterpret_cast<uint4*>(dst);

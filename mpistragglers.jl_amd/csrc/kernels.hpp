@@ -54,7 +54,12 @@ struct LsqTask {
   uint32_t base0, base1;
   int64_t rows, lda;
   int cols, grid;
+  // pre-armed launch of a worker process: device copy of the doorbell the
+  // launch waited on; a value with kCancelBit set means "disarmed", and the task returns
+  // without computing or publishing (NULL: not armed)
+  const unsigned long long* go;
 };
+constexpr unsigned long long kCancelBit = 1ull << 62;
 
 // Several workers dispatched by the same flush run as ONE launch: workgroups
 // [block0[t], block0[t+1]) belong to task t.  All tasks share (dtype, cols_pad).
@@ -97,6 +102,7 @@ struct LsqbTask {
   int grid1;           // pass-1 workgroups (256 rows each, grid-strided)
   int nrange, nslice;  // pass-2 grid = nrange * nslice
   uint32_t sbase, tbase;  // ctr values before this launch (every slice counter moves alike)
+  const unsigned long long* go;  // as LsqTask::go
 };
 struct LsqbBatch {
   int ntasks;

@@ -140,6 +140,11 @@ struct HipWorker {
   uint8_t* box_reply_dev = nullptr;
   unsigned long long* box_door_dev = nullptr;
   uint8_t* xslot = nullptr;  // server: device copy of the staged message
+  // server, pre-armed task (serve()): armed = task `seq` is queued behind its doorbell;
+  // go_dev = device copy of the doorbell it ran on; counter bases to restore if cancelled
+  bool armed = false;
+  unsigned long long* go_dev = nullptr;
+  uint32_t arm_ctr0 = 0, arm_ctr1 = 0, arm_sbase = 0, arm_tbase = 0;
 };
 
 // Accumulates copy items and doorbells into as few exchange launches as fit the kernel
@@ -266,6 +271,10 @@ class HipComm final : public Comm {
   }
 
   ~HipComm() override {
+    try {
+      disarm_all();
+    } catch (...) {
+    }
     stop_timer();
     (void)hipDeviceSynchronize();
     for (auto& w : w_) {
@@ -274,6 +283,7 @@ class HipComm final : public Comm {
       if (w.lsqb_slab) (void)hipFree(w.lsqb_slab);
       if (w.lsqb_ctr) (void)hipFree(w.lsqb_ctr);
       if (w.xslot) (void)hipFree(w.xslot);
+      if (w.go_dev) (void)hipFree(w.go_dev);
       if (w.stream) release_queue_stream(dev_, w.stream);
     }
     for (auto& s : launch_streams_) release_queue_stream(dev_, s);
@@ -431,18 +441,42 @@ class HipComm final : public Comm {
   }
 
   // ---- worker process: watch the doorbells of the workers served here ----
+  // Least-squares workers without a delay schedule are PRE-ARMED: their next task is
+  // already queued on the worker's own stream behind hipStreamWaitValue64 on the mailbox
+  // doorbell, so the GPU starts it when rank 0's exchange kernel rings (3.2 us ring -> task
+  // start, against 13.4 us for host polling + launch; profiles/r01_probe_waitvalue.txt).
+  // Other workers (the reference's test programs, injected delays) are launched by this
+  // thread when it sees their doorbell.  serve() returns at pause / shutdown after
+  // disarming: the pending waits are released with kCancelBit and their tasks return
+  // without computing or publishing.
   void serve() {
     if (role_ != SERVER) fail(MPA_ERROR, "mpa_comm_serve is for worker processes (rank != 0)");
     ShmHeader* h = region_->header();
     const uint64_t gen0 = __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE);
     const auto t0 = Clock::now();
+    struct Disarm {
+      HipComm* c;
+      ~Disarm() { c->disarm_all(); }
+    } disarm_guard{this};
     std::vector<int64_t> fresh;
+    for (int64_t r = 1; r <= nworkers_; ++r)
+      if (w_[size_t(r - 1)].here && armable(r)) arm(r);
     for (uint64_t spins = 0;; ++spins) {
       if (__atomic_load_n(&h->shutdown, __ATOMIC_ACQUIRE) || __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE) != gen0) break;
       fresh.clear();
+      bool progress = false;
       for (int64_t r = 1; r <= nworkers_; ++r) {
         HipWorker& w = w_[size_t(r - 1)];
         if (!w.here) continue;
+        if (w.armed) {
+          if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) continue;
+          // the armed task ran: check what rank 0 posted against what it was armed for
+          w.armed = false;
+          check_task(r, tasks_[size_t(r - 1)], size_t(w.box->msg_bytes), size_t(w.box->reply_bytes));
+          progress = true;
+          if (armable(r)) arm(r);
+          continue;
+        }
         const unsigned long long db = __atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE);
         if (db == w.seq) continue;
         if (db != w.seq + 1) fail(MPA_ERROR, "mailbox protocol: worker %lld doorbell %llu after %llu", (long long)r, db, w.seq);
@@ -459,10 +493,87 @@ class HipComm final : public Comm {
       if (!fresh.empty()) {
         if (timing_) reap_timing(false);
         launch_tasks(fresh, /*staged=*/true);
-      } else {
+      } else if (!progress) {
         if ((spins & 0xFFF) == 0xFFF) watchdog(t0, /*timeout=*/false);
         __builtin_ia32_pause();
       }
+    }
+  }
+
+  // ---- pre-armed tasks (server) ----
+  bool armable(int64_t rank) const {
+    const TaskSpec& ts = tasks_[size_t(rank - 1)];
+    return (ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty();
+  }
+
+  // message / reply bytes of a task as armed (the post is checked against them afterwards)
+  static size_t task_msg_bytes(const TaskSpec& ts) {
+    return ts.kind == MPA_TASK_LSQ_BATCH ? size_t(ts.cols) * size_t(ts.k) * 2
+                                         : size_t(ts.cols) * (ts.dtype == MPA_F64 ? 8 : 4);
+  }
+
+  // queue task seq+1 of `rank` on its stream: wait for the doorbell, stage the message and
+  // the doorbell value (the task's go word), run the task
+  void arm(int64_t rank) {
+    HipWorker& w = w_[size_t(rank - 1)];
+    const TaskSpec& ts = tasks_[size_t(rank - 1)];
+    if (!w.go_dev) {
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.go_dev), 64));
+      HIPCHECK(hipMemset(w.go_dev, 0, 64));
+    }
+    const unsigned long long s = w.seq + 1;
+    w.arm_ctr0 = w.ctr0;
+    w.arm_ctr1 = w.ctr1;
+    w.arm_sbase = w.lsqb_sbase;
+    w.arm_tbase = w.lsqb_tbase;
+    HIPCHECK(hipStreamWaitValue64(w.stream, w.box_door_dev, s, hipStreamWaitValueGte, ~0ull));
+    w.seq = s;
+    w.sl = task_msg_bytes(ts);
+    w.rl = w.sl * (ts.kind == MPA_TASK_LSQ_BATCH ? 2 : 1);
+    w.x = w.xslot;
+    w.out = w.box_reply_dev;
+    ExchangeBuilder xb(ticket_, &ticket_count_, w.stream);
+    xb.copy(w.box_msg_dev, w.xslot, w.sl);
+    xb.copy(reinterpret_cast<const uint8_t*>(w.box_door_dev), reinterpret_cast<uint8_t*>(w.go_dev), 8);
+    xb.launch();
+    double bytes = 0;
+    if (ts.kind == MPA_TASK_LSQ) {
+      LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes);
+      b.t[0].go = w.go_dev;
+      enqueue_lsq(b, ts.dtype, int(ts.cols), w.stream, bytes, rank);
+    } else {
+      LsqbBatch b = build_lsqb_batch({rank}, &bytes);
+      b.t[0].go = w.go_dev;
+      enqueue_lsqb(b, w.stream, bytes, rank);
+    }
+    w.armed = true;
+  }
+
+  // release every pending armed wait: a task whose doorbell rank 0 has not rung is
+  // cancelled (doorbell := seq | kCancelBit, then restored), one already rung completes
+  void disarm_all() {
+    if (role_ != SERVER) return;
+    for (int64_t r = 1; r <= nworkers_; ++r) {
+      HipWorker& w = w_[size_t(r - 1)];
+      if (!w.here || !w.armed) continue;
+      unsigned long long expect = w.seq - 1;
+      const unsigned long long cancel = w.seq | kCancelBit;
+      const bool cancelled = __atomic_compare_exchange_n(&w.box->doorbell, &expect, cancel, false, __ATOMIC_ACQ_REL,
+                                                         __ATOMIC_ACQUIRE);
+      (void)hipStreamSynchronize(w.stream);
+      if (cancelled) {
+        unsigned long long c2 = cancel;  // restore unless rank 0 rang meanwhile
+        __atomic_compare_exchange_n(&w.box->doorbell, &c2, w.seq - 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+      }
+      if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) {  // it did not run
+        w.seq -= 1;
+        w.ctr0 = w.arm_ctr0;
+        w.ctr1 = w.arm_ctr1;
+        w.lsqb_sbase = w.arm_sbase;
+        w.lsqb_tbase = w.arm_tbase;
+        void_timing(r);
+      }
+      w.armed = false;
     }
   }
 
@@ -938,7 +1049,7 @@ class HipComm final : public Comm {
     return b;
   }
 
-  void enqueue_lsqb(const LsqbBatch& b, hipStream_t s, double bytes) {
+  void enqueue_lsqb(const LsqbBatch& b, hipStream_t s, double bytes, int64_t armed_rank = 0) {
     TimedLaunch tl{};
     const bool timed = timing_;
     if (timed) {
@@ -946,6 +1057,7 @@ class HipComm final : public Comm {
       tl.start = take_event();
       tl.stop = take_event();
       tl.bytes = bytes;
+      tl.rank = armed_rank;
       HIPCHECK(hipEventRecord(tl.start, s));
     }
     HIPCHECK(launch_lsqb(b, s));
@@ -957,7 +1069,7 @@ class HipComm final : public Comm {
   }
 
   // enqueue one least-squares launch on `s` (coordinator / server thread or timer thread)
-  void enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes) {
+  void enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes, int64_t armed_rank = 0) {
     TimedLaunch tl{};
     const bool timed = timing_;
     if (timed) {
@@ -965,6 +1077,7 @@ class HipComm final : public Comm {
       tl.start = take_event();
       tl.stop = take_event();
       tl.bytes = bytes;
+      tl.rank = armed_rank;
     }
     if (timed) HIPCHECK(hipEventRecord(tl.start, s));
     if (debug_) {
@@ -1013,7 +1126,19 @@ class HipComm final : public Comm {
   struct TimedLaunch {
     hipEvent_t start, stop;
     double bytes;
+    int64_t rank;  // pre-armed launch of this worker (0: none)
+    bool void_ = false;  // cancelled before it ran: not counted
   };
+
+  // the pending timed launch armed for `rank` was cancelled
+  void void_timing(int64_t rank) {
+    std::lock_guard<std::mutex> lk(tm_mu_);
+    for (auto it = timed_.rbegin(); it != timed_.rend(); ++it)
+      if (it->rank == rank && !it->void_) {
+        it->void_ = true;
+        break;
+      }
+  }
 
   hipEvent_t take_event() {
     if (!event_pool_.empty()) {
@@ -1037,11 +1162,13 @@ class HipComm final : public Comm {
         timed_[keep++] = tl;
         continue;
       }
-      float ms = 0;
-      HIPCHECK(hipEventElapsedTime(&ms, tl.start, tl.stop));
-      t_ms_ += ms;
-      t_bytes_ += tl.bytes;
-      t_launches_ += 1;
+      if (!tl.void_) {
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, tl.start, tl.stop));
+        t_ms_ += ms;
+        t_bytes_ += tl.bytes;
+        t_launches_ += 1;
+      }
       event_pool_.push_back(tl.start);
       event_pool_.push_back(tl.stop);
     }

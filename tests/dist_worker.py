@@ -173,3 +173,145 @@ def lsq_dist(rank, world, port, placement, result_q):
     except Exception:
         result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
         raise
+
+
+def lsq_dist_armed(rank, world, port, placement, delayed, result_q):
+    """Pre-armed serving (workers without a delay schedule wait on their doorbell inside
+    the GPU queue): two serve sessions with a pause between them (armed tasks cancelled and
+    re-armed), nwait = n then nwait = 2 with stale results, every chunk checked against the
+    fp64 gradient of the iterate of its epoch."""
+    import numpy as np
+    try:
+        dist = _init(rank, world, port)
+        import torch
+        torch.cuda.set_device(0)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import mpiasyncpools as M
+        n, rows, cols, seed = len(placement), 3000, 512, 23
+        name = [f"/mpa_a{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+        if rank == 0:
+            comm = M.DistComm(n, placement, 0, name[0], cols * 4, transport="hip")
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            comm = M.DistComm(n, placement, rank, name[0], cols * 4, transport="hip")
+        keep = []
+        for w in range(1, n + 1):
+            if placement[w - 1] == rank:
+                A = torch.empty(rows, cols, device="cuda")
+                b = torch.empty(rows, device="cuda")
+                M.generate(A, seed, 0, (w - 1) * rows * cols, float(np.float32(1 / np.sqrt(cols))))
+                M.generate(b, seed, 1, (w - 1) * rows, 1.0)
+                keep.append((A, b))
+                comm.set_task_lsq(w, A, b)
+                if w in delayed:
+                    comm.set_delays(w, [3_000_000, 0, 1_000_000])
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank != 0:
+            for _ in range(2):
+                comm.serve()
+                dist.barrier()
+            comm.close()
+            dist.destroy_process_group()
+            return
+        import lsq
+        A_all = lsq.gen_matrix(seed, 0, n * rows, cols, "f32")
+        b_all = lsq.gen_vector(seed, 0, n * rows, "f32")
+        pool = M.MPIAsyncPool(n)
+        x = torch.zeros(cols, device="cuda")
+        isend = torch.zeros(n * cols, device="cuda")
+        recv = torch.zeros(n * cols, device="cuda")
+        irecv = torch.zeros_like(recv)
+        sent, errors = {}, []
+        for session, nwait in ((1, n), (2, 2)):
+            for _ in range(6):
+                epoch = pool.epoch + 1
+                sent[epoch] = x.cpu().numpy().copy()
+                rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=nwait)
+                ch = recv.cpu().numpy().reshape(n, cols)
+                if int((rep == epoch).sum()) < nwait:
+                    errors.append(("fresh", session, epoch, rep.tolist()))
+                for i in range(n):
+                    if rep[i] == 0:
+                        continue
+                    g = lsq.shard_gradient(A_all[i * rows:(i + 1) * rows], b_all[i * rows:(i + 1) * rows],
+                                           sent[int(rep[i])])
+                    e = lsq.rel_err(ch[i], g)
+                    if not e <= 1e-5:
+                        errors.append(("grad", session, epoch, i, int(rep[i]), e))
+                w = (rep == epoch).astype(np.float64) * (n / max(1, int((rep == epoch).sum())))
+                comm.lsq_update(x, recv, n, w, 0.05)
+            M.waitall_(pool, recv, irecv)
+            if session == 1:
+                comm.pause_servers()
+                dist.barrier()
+        comm.shutdown()
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        result_q.put(("ok", errors))
+    except Exception:
+        result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
+        raise
+
+
+def lsqb_dist(rank, world, port, placement, result_q):
+    """The batched 64-iterate variant across processes (pre-armed on the serving rank)."""
+    import numpy as np
+    try:
+        dist = _init(rank, world, port)
+        import torch
+        torch.cuda.set_device(0)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import mpiasyncpools as M
+        import lsq
+        n, rows, cols, K, seed = len(placement), 1000, 256, 64, 29
+        name = [f"/mpa_b{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+        if rank == 0:
+            comm = M.DistComm(n, placement, 0, name[0], cols * K * 4, transport="hip")
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            comm = M.DistComm(n, placement, rank, name[0], cols * K * 4, transport="hip")
+        A_all = lsq.gen_matrix(seed, 0, n * rows, cols, "bf16")
+        B_all = lsq.gen_matrix(seed, 0, n * rows, K, "bf16", stream=lsq.STREAM_B, scale=np.float32(1.0))
+
+        def bf16(bits):
+            return torch.from_numpy(np.ascontiguousarray(bits).view(np.int16)).cuda().view(torch.bfloat16)
+        keep = []
+        for w in range(1, n + 1):
+            if placement[w - 1] == rank:
+                A, B = bf16(A_all[(w - 1) * rows:w * rows]), bf16(B_all[(w - 1) * rows:w * rows])
+                keep.append((A, B))
+                comm.set_task_lsq_batch(w, A, B)
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank != 0:
+            comm.serve()
+            dist.barrier()
+            comm.close()
+            dist.destroy_process_group()
+            return
+        pool = M.MPIAsyncPool(n)
+        send = torch.zeros(cols * K, dtype=torch.bfloat16, device="cuda")
+        isend = torch.zeros(n * cols * K, dtype=torch.bfloat16, device="cuda")
+        recv = torch.zeros(n * cols * K, device="cuda")
+        irecv = torch.zeros_like(recv)
+        errors = []
+        for epoch in range(1, 5):
+            X = lsq.gen_matrix(300 + epoch, 0, cols, K, "bf16", stream=lsq.STREAM_X, scale=np.float32(0.5))
+            send.copy_(bf16(X).view(-1))
+            M.asyncmap_(pool, send, recv, isend, irecv, comm, nwait=n)
+            ch = recv.cpu().numpy().reshape(n, cols, K)
+            for i in range(n):
+                G = lsq.batched_shard_gradient(A_all[i * rows:(i + 1) * rows], B_all[i * rows:(i + 1) * rows], X)
+                e = lsq.rel_err(ch[i], G)
+                if not e <= 1e-4:
+                    errors.append(("G", epoch, i, e))
+        comm.shutdown()
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        result_q.put(("ok", errors))
+    except Exception:
+        result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
+        raise

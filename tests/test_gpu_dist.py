@@ -42,3 +42,19 @@ def test_lsq_two_processes_hip(built):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run(dist_worker.lsq_dist, 2, [0, 1, 1, 1])
+
+
+def test_lsq_two_processes_prearmed(built):
+    """Workers 2-4 on rank 1: 2 and 3 pre-armed (no delays), 4 delayed (host-launched);
+    two serve sessions around a pause."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.lsq_dist_armed, 2, [0, 1, 1, 1], [4])
+
+
+def test_lsqb_two_processes_prearmed(built):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.lsqb_dist, 2, [0, 1])
