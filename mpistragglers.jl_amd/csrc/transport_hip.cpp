@@ -260,6 +260,8 @@ class HipComm final : public Comm {
     rt_hz_ = khz > 0 ? double(khz) * 1e3 : 100e6;
     const char* t = std::getenv("MPA_WAIT_TIMEOUT_S");
     timeout_s_ = t ? std::atof(t) : 600.0;
+    const char* arm = std::getenv("MPA_ARM");  // 0: worker processes launch every task on its doorbell
+    arm_enabled_ = !(arm && *arm == '0');
     const char* dbg = std::getenv("MPA_DEBUG");
     debug_ = dbg && *dbg == '1';
     if (debug_ && region_) {
@@ -503,7 +505,13 @@ class HipComm final : public Comm {
   // ---- pre-armed tasks (server) ----
   bool armable(int64_t rank) const {
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
-    return (ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty();
+    return arm_enabled_ && (ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty();
+  }
+  // local workers that serve() pre-arms: each armed launch gets its share of the launch grid
+  int armed_share() const {
+    int k = 0;
+    for (int64_t r = 1; r <= nworkers_; ++r) k += w_[size_t(r - 1)].here && armable(r);
+    return k > 0 ? k : 1;
   }
 
   // message / reply bytes of a task as armed (the post is checked against them afterwards)
@@ -538,7 +546,7 @@ class HipComm final : public Comm {
     xb.launch();
     double bytes = 0;
     if (ts.kind == MPA_TASK_LSQ) {
-      LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes);
+      LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes, armed_share());
       b.t[0].go = w.go_dev;
       enqueue_lsq(b, ts.dtype, int(ts.cols), w.stream, bytes, rank);
     } else {
@@ -950,9 +958,12 @@ class HipComm final : public Comm {
   }
 
   // kernel arguments of one launch over `ranks`; advances their arrival-counter bases
-  LsqBatch build_lsq_batch(const std::vector<int64_t>& ranks, int dtype, double* bytes_out) {
+  // `share`: the launch grid is divided as if this many tasks ran at once (concurrent
+  // single-task launches of pre-armed workers)
+  LsqBatch build_lsq_batch(const std::vector<int64_t>& ranks, int dtype, double* bytes_out, int share = 0) {
     LsqBatch b{};
     b.ntasks = int(ranks.size());
+    const int split = share > b.ntasks ? share : b.ntasks;
     b.err = err_dev_;
     b.spin_ticks = spin_ticks();
     int blocks = 0;
@@ -973,7 +984,7 @@ class HipComm final : public Comm {
       t.rows = ts.rows;
       t.lda = ts.lda;
       t.cols = int(ts.cols);
-      t.grid = lsq_grid(ts, w, b.ntasks);
+      t.grid = lsq_grid(ts, w, split);
       t.base0 = w.ctr0;
       t.base1 = w.ctr1;
       w.ctr0 += uint32_t(t.grid);
@@ -1195,6 +1206,7 @@ class HipComm final : public Comm {
   CallBufs b_;
   bool timing_ = false;
   bool debug_ = false;
+  bool arm_enabled_ = true;
   std::vector<TimedLaunch> timed_;
   std::vector<hipEvent_t> event_pool_;
   int64_t t_launches_ = 0;
