@@ -260,8 +260,8 @@ class HipComm final : public Comm {
     rt_hz_ = khz > 0 ? double(khz) * 1e3 : 100e6;
     const char* t = std::getenv("MPA_WAIT_TIMEOUT_S");
     timeout_s_ = t ? std::atof(t) : 600.0;
-    const char* arm = std::getenv("MPA_ARM");  // 0: worker processes launch every task on its doorbell
-    arm_enabled_ = !(arm && *arm == '0');
+    const char* arm = std::getenv("MPA_ARM");  // unset: auto (armable(); 0 never, 1 always)
+    arm_mode_ = arm && *arm == '0' ? 0 : arm && *arm == '1' ? 1 : 2;
     const char* dbg = std::getenv("MPA_DEBUG");
     debug_ = dbg && *dbg == '1';
     if (debug_ && region_) {
@@ -503,9 +503,18 @@ class HipComm final : public Comm {
   }
 
   // ---- pre-armed tasks (server) ----
+  // Pre-arming pays where a process serves ONE worker (one worker per GPU, N = 8): with
+  // several, the host-launched path batches them into one launch, which measured faster
+  // than concurrent single-task armed launches (N = 2 rehearsal on one GPU: 1280 vs 1175
+  // it/s, profiles/r01_n2_arm_ab.txt).  MPA_ARM=1 arms every eligible worker, MPA_ARM=0 none.
   bool armable(int64_t rank) const {
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
-    return arm_enabled_ && (ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty();
+    if (arm_mode_ == 0 || !((ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty()))
+      return false;
+    if (arm_mode_ == 1) return true;
+    int here = 0;
+    for (const auto& w : w_) here += w.here;
+    return here == 1;
   }
   // local workers that serve() pre-arms: each armed launch gets its share of the launch grid
   int armed_share() const {
@@ -1206,7 +1215,7 @@ class HipComm final : public Comm {
   CallBufs b_;
   bool timing_ = false;
   bool debug_ = false;
-  bool arm_enabled_ = true;
+  int arm_mode_ = 2;
   std::vector<TimedLaunch> timed_;
   std::vector<hipEvent_t> event_pool_;
   int64_t t_launches_ = 0;
