@@ -95,6 +95,14 @@ def step_size(rows, cols):
 TORCH_DT = {"f32": "float32", "f64": "float64", "bf16": "bfloat16"}
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A line on stderr per phase: long configs (c3-c5 generate 32-128 GiB) never go silent."""
+    print("[bench %.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
 def gen_shard(M, torch, cfg, seed, w):
     """Rows of worker w (1-based) of the global synthetic problem, on the current GPU
     (b: rows; the batched variant's B: rows x 64)."""
@@ -192,6 +200,8 @@ def run_single(args, cfg):
     batched = k > 1
     comm = M.DeviceComm(n)
     shards = [gen_shard(M, torch, cfg, args.seed, w) for w in range(1, n + 1)]
+    torch.cuda.synchronize()
+    progress("generated %d shards (%s)" % (n, cfg["config"]))
     for w, (A, b) in enumerate(shards, start=1):
         if batched:
             comm.set_task_lsq_batch(w, A, b)
@@ -243,6 +253,7 @@ def run_single(args, cfg):
     # timed region: the coordinator loop in native code (mpa_lsq_descent / mpa_lsqb_descent)
     loop(args.warmup)
     torch.cuda.synchronize()
+    progress("warmup done (%d epochs)" % args.warmup)
     comm.timing()
     comm.set_timing(True)
     torch.cuda.synchronize()

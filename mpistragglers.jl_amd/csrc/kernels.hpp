@@ -45,13 +45,10 @@ struct LsqTask {
   const void* b;
   const void* x;
   void* out;
-  void* slab;       // [grid][cols_pad] partial sums (T)
-  uint32_t* ctr;    // [2] monotonic arrival counters (device memory)
+  void* slab;       // [grid][cols_pad] partial sums (T), reduced in place
+  uint32_t* ctr;    // [kLsqCtrPerTask] reduction-tree arrival counters, zero between launches
   unsigned long long* flag;  // host-pinned completion word of the worker
   unsigned long long seq;
-  // ctr[0] / ctr[1] values before this launch.  Launch grids vary with the batch a task
-  // lands in, so the host keeps the running totals (not seq * grid).
-  uint32_t base0, base1;
   int64_t rows, lda;
   int cols, grid;
   // pre-armed launch of a worker process: device copy of the doorbell the
@@ -60,6 +57,12 @@ struct LsqTask {
   const unsigned long long* go;
 };
 constexpr unsigned long long kCancelBit = 1ull << 62;
+
+// Reduction tree of a least-squares task (lsq_kernel.hip): fan-in, most workgroups per
+// task, and the counters it needs (level l has ceil(kLsqMaxGrid / 8^(l+1)) groups).
+constexpr int kLsqFanIn = 8;
+constexpr int kLsqMaxGrid = 1024;
+constexpr int kLsqCtrPerTask = 160;  // 128 + 16 + 2 + 1, rounded up
 
 // Several workers dispatched by the same flush run as ONE launch: workgroups
 // [block0[t], block0[t+1]) belong to task t.  All tasks share (dtype, cols_pad).
@@ -77,7 +80,6 @@ const char* lsq_variant_name();  // the c2-shape kernel variant in use (MPA_LSQ_
 int lsq_set_variant(int i);      // returns the number of variants, or -1 if i is out of range
 // Shape helpers for the launcher's variant table.
 int lsq_cols_pad(int dtype, int cols);  // 0 if unsupported
-int lsq_reducers(int dtype, int cols);
 int lsq_rows_per_wave_iter(int dtype, int cols);
 
 // One worker task of the batched multi-iterate variant (lsqb_kernel.hip):

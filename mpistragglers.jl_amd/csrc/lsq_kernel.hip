@@ -13,10 +13,10 @@
 //
 // Cross-workgroup reduction, deterministic (no float atomics): the 4 waves of a
 // workgroup add their g in LDS in wave order, the workgroup stores its partial into
-// slab[block][:], and takes a ticket on a monotonic arrival counter.  The last R arrivers
-// (R = 4*VPL) each wait until the counter reaches the grid, then sum one 256-B column block
-// of the slab over all workgroups in block order into the reply chunk; the last of them
-// publishes completion.  Every in-kernel wait is bounded (spin_ticks).
+// slab[block][:], and a fan-in-8 tree of arrival counters sums the partials in block
+// order: the last arriver of each group of 8 carries the group's sum one level up, the
+// last one writes the reply chunk and publishes completion.  Nothing waits on another
+// workgroup, so the result never depends on how many workgroups are resident.
 //
 // Compile-time variants (MODE bits) exist for measurement (DESIGN.md §Kernel tuning):
 //   M_CLAMP     branch-free loads: out-of-range rows/vectors read a clamped in-bounds
@@ -175,9 +175,7 @@ template <typename T, int VPL, int RB, int MODE>
 __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   using P = Pack<T>;
   constexpr int E = P::E;
-  constexpr int R = 4 * VPL;            // reducers; each owns 16 vectors = 256 B of columns
   __shared__ P red[VPL * 64];           // workgroup partial (VPL*64*E columns)
-  __shared__ P part[16][16];            // reducer phase partials
   __shared__ unsigned s_ticket;
 
   // which task of the batch this workgroup serves (wave-uniform scan over <= 16 entries)
@@ -249,94 +247,79 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     }
     __syncthreads();
   }
-  P* slab = static_cast<P*>(a.slab) + size_t(blk) * (VPL * 64);
-  for (int j = tid; j < VPL * 64; j += kThreads) slab[j] = red[j];
-  drain_vm();
-  __syncthreads();
-
+  // Cross-workgroup reduction: a fan-in-8 tree over the workgroup partials, with no
+  // waiting.  Level l groups 8 consecutive level-l partials; the member that arrives LAST
+  // at its group's counter (release before the add, acquire after it) sums the group in
+  // member order and carries the result to level l+1; the others return.  A workgroup
+  // only ever reads partials whose writers have already arrived, so the tree completes
+  // whatever the residency (concurrent launches of delayed workers filled the chip with
+  // spinning reducers under the earlier wait-for-all scheme: fp64, 2048 columns, 8
+  // concurrent single-task launches ran 1000x slow).  Partials stay in place: the level-l
+  // partial of element e sits in slab row e * 8^l; each counter is reset by its group's
+  // last arriver, and the next launch of the worker is stream-ordered after this one.
+  constexpr int S = VPL * 64;  // 16-B vectors per partial
+  constexpr unsigned F = kLsqFanIn;
+  P* __restrict__ slab = static_cast<P*>(a.slab);
+  T* __restrict__ out = static_cast<T*>(a.out);
   const unsigned G = unsigned(a.grid);
-  const unsigned base0 = a.base0;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    drain_vm();
-    const unsigned old = __hip_atomic_fetch_add(&a.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_ticket = old - base0;
-  }
-  __syncthreads();
-  const unsigned ticket = s_ticket;
-  if (ticket + R < G) return;  // not one of the last R arrivers
-  const int k = int(ticket + R - G);  // reducer index 0..R-1
-
-  if (tid == 0) {
-    const unsigned long long t0 = rt_now();
-    while (__hip_atomic_load(&a.ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base0 < G) {
-      __builtin_amdgcn_s_sleep(2);
-      if (rt_now() - t0 > batch.spin_ticks) {
-        __hip_atomic_fetch_or(batch.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    drain_vm();
-  }
-  __syncthreads();
-
-  // column block k: vectors [16k, 16k+16) of every slab row, summed over blocks in order
-  const int vv = tid & 15, ph = tid >> 4;
-  // four independent accumulators keep four slab loads in flight per thread (the sum is
-  // latency-bound otherwise); combined in a fixed order, so the result is still bitwise
-  // reproducible for a given grid
-  const P* src = static_cast<const P*>(a.slab) + k * 16 + vv;
-  constexpr size_t S = VPL * 64;
-  P acc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int e = 0; e < E; ++e) acc[q].v[e] = T(0);
-  unsigned b = unsigned(ph);
-  for (; b + 48 < G; b += 64) {
-    P t[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) t[q] = src[size_t(b + 16 * q) * S];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[q].v[e] += t[q].v[e];
-  }
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    if (b < G) {
-      const P t = src[size_t(b) * S];
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[q].v[e] += t.v[e];
-      b += 16;
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < E; ++e) acc[0].v[e] = (acc[0].v[e] + acc[1].v[e]) + (acc[2].v[e] + acc[3].v[e]);
-  part[ph][vv] = acc[0];
-  __syncthreads();
-  if (ph == 0) {
-    P s = part[0][vv];
-#pragma unroll
-    for (int q = 1; q < 16; ++q)
-#pragma unroll
-      for (int e = 0; e < E; ++e) s.v[e] += part[q][vv].v[e];
-    T* out = static_cast<T*>(a.out);
-    const int c0 = (k * 16 + vv) * E;
+  auto store_out = [&](int j, const P& s) {
+    const int c0 = j * E;
 #pragma unroll
     for (int e = 0; e < E; ++e)
       if (c0 + e < a.cols) out[c0 + e] = s.v[e];
+  };
+  if (G == 1) {
+    for (int j = tid; j < S; j += kThreads) store_out(j, red[j]);
+  } else {
+    for (int j = tid; j < S; j += kThreads) slab[size_t(blk) * S + j] = red[j];
+    unsigned idx = unsigned(blk), count = G, stride = 1;
+    int lvl_off = 0, lvl_cap = kLsqMaxGrid / int(F);
+    for (;;) {
+      drain_vm();
+      __syncthreads();
+      const unsigned first = (idx / F) * F;
+      const unsigned gsize = count - first < F ? count - first : F;
+      if (tid == 0) {
+        unsigned* c = &a.ctr[lvl_off + int(idx / F)];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        drain_vm();
+        const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ticket = old + 1 == gsize;
+        if (s_ticket) {
+          __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          drain_vm();
+        }
+      }
+      __syncthreads();
+      if (!s_ticket) return;  // an earlier arriver of the group: the last one carries it
+      const unsigned next = (count + F - 1) / F;
+      const P* src = slab + size_t(first) * stride * S;
+      for (int j = tid; j < S; j += kThreads) {
+        P t[F];
+#pragma unroll
+        for (unsigned m = 0; m < F; ++m)
+          if (m < gsize) t[m] = src[size_t(m) * stride * S + j];
+        P s = t[0];
+#pragma unroll
+        for (unsigned m = 1; m < F; ++m)
+          if (m < gsize)
+#pragma unroll
+            for (int e = 0; e < E; ++e) s.v[e] += t[m].v[e];
+        if (next == 1) store_out(j, s);
+        else slab[size_t(first) * stride * S + j] = s;
+      }
+      if (next == 1) break;
+      idx /= F;
+      count = next;
+      stride *= F;
+      lvl_off += lvl_cap;
+      lvl_cap = (lvl_cap + int(F) - 1) / int(F);
+    }
   }
   drain_vm();
   __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    drain_vm();
-    const unsigned base1 = a.base1;
-    const unsigned old = __hip_atomic_fetch_add(&a.ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old - base1 == unsigned(R - 1)) publish_done(a.flag, a.seq);
-  }
+  if (tid == 0) publish_done(a.flag, a.seq);
 }
 
 template <typename T, int VPL, int RB, int MODE>
@@ -403,11 +386,6 @@ int lsq_cols_pad(int dtype, int cols) {
     return vp * 64 * 2;
   }
   return 0;
-}
-
-int lsq_reducers(int dtype, int cols) {
-  const int cp = lsq_cols_pad(dtype, cols);
-  return cp ? 4 * (cp / (64 * (dtype == MPA_F64 ? 2 : 4))) : 0;
 }
 
 int lsq_rows_per_wave_iter(int dtype, int cols) {

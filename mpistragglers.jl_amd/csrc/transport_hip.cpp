@@ -58,7 +58,7 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 constexpr int kDefaultLaunchGrid = 512;  // 2 workgroups per CU: profiles/r01_tune_sweep2.jsonl
-constexpr int kSlabGridCap = 1024;       // most workgroups a single task may be given
+constexpr int kSlabGridCap = kLsqMaxGrid;  // most workgroups a single task may be given
 constexpr int kLaunchStreams = 2;
 // batched multi-iterate task: pass-1 / pass-2 workgroups per launch (= resident: 1 x 512 /
 // 2 x 256 threads per CU by VGPRs), and the most row ranges a pass-2 task is split into
@@ -118,7 +118,6 @@ struct HipWorker {
   unsigned long long seq = 0;  // coordinator: tasks posted; server: tasks served
   void* slab = nullptr;
   int slab_grid = 0;
-  uint32_t ctr0 = 0, ctr1 = 0;  // running totals of this worker's two arrival counters
   // batched multi-iterate task (lsqb_kernel.hip): residual scratch, pass-2 partials,
   // counters and their running totals
   void* lsqb_R = nullptr;
@@ -144,7 +143,7 @@ struct HipWorker {
   // go_dev = device copy of the doorbell it ran on; counter bases to restore if cancelled
   bool armed = false;
   unsigned long long* go_dev = nullptr;
-  uint32_t arm_ctr0 = 0, arm_ctr1 = 0, arm_sbase = 0, arm_tbase = 0;
+  uint32_t arm_sbase = 0, arm_tbase = 0;
 };
 
 // Accumulates copy items and doorbells into as few exchange launches as fit the kernel
@@ -225,8 +224,8 @@ class HipComm final : public Comm {
     std::memset(flags_, 0, sizeof(unsigned long long) * size_t(n + 1));
     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&err_), 64, hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(err_, 0, 64);
-    HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (2 * size_t(n) + 1)));
-    HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (2 * size_t(n) + 1)));
+    HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 1)));
+    HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 1)));
     err_dev_ = err_;
     if (region_) {
       if (region_->nworkers() != n) fail(MPA_ARGUMENT_ERROR, "shared memory holds %lld workers, comm has %lld",
@@ -539,8 +538,6 @@ class HipComm final : public Comm {
       HIPCHECK(hipMemset(w.go_dev, 0, 64));
     }
     const unsigned long long s = w.seq + 1;
-    w.arm_ctr0 = w.ctr0;
-    w.arm_ctr1 = w.ctr1;
     w.arm_sbase = w.lsqb_sbase;
     w.arm_tbase = w.lsqb_tbase;
     HIPCHECK(hipStreamWaitValue64(w.stream, w.box_door_dev, s, hipStreamWaitValueGte, ~0ull));
@@ -584,8 +581,6 @@ class HipComm final : public Comm {
       }
       if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) {  // it did not run
         w.seq -= 1;
-        w.ctr0 = w.arm_ctr0;
-        w.ctr1 = w.arm_ctr1;
         w.lsqb_sbase = w.arm_sbase;
         w.lsqb_tbase = w.arm_tbase;
         void_timing(r);
@@ -730,12 +725,11 @@ class HipComm final : public Comm {
   int lsq_grid(const TaskSpec& ts, const HipWorker& w, int ntasks) const {
     const int total = g_lsq_grid > 0 ? g_lsq_grid : kDefaultLaunchGrid;
     const int rpw = lsq_rows_per_wave_iter(ts.dtype, int(ts.cols));
-    const int R = lsq_reducers(ts.dtype, int(ts.cols));
     const int64_t want = (ts.rows + 4 * rpw - 1) / (4 * rpw);
     int g = total / (ntasks > 0 ? ntasks : 1);
     if (g > want) g = int(want);
     if (g > w.slab_grid) g = w.slab_grid;
-    if (g < R) g = R;
+    if (g < 1) g = 1;
     return g;
   }
 
@@ -966,7 +960,7 @@ class HipComm final : public Comm {
     enqueue_lsq(b, dtype, int(tasks_[size_t(ranks[0] - 1)].cols), s, bytes);
   }
 
-  // kernel arguments of one launch over `ranks`; advances their arrival-counter bases
+  // kernel arguments of one launch over `ranks`
   // `share`: the launch grid is divided as if this many tasks ran at once (concurrent
   // single-task launches of pre-armed workers)
   LsqBatch build_lsq_batch(const std::vector<int64_t>& ranks, int dtype, double* bytes_out, int share = 0) {
@@ -987,17 +981,13 @@ class HipComm final : public Comm {
       t.x = w.x;
       t.out = w.out;
       t.slab = w.slab;
-      t.ctr = ctr_ + 2 * (rank - 1);
+      t.ctr = ctr_ + kLsqCtrPerTask * (rank - 1);
       t.flag = w.flag_dev;
       t.seq = w.seq;
       t.rows = ts.rows;
       t.lda = ts.lda;
       t.cols = int(ts.cols);
       t.grid = lsq_grid(ts, w, split);
-      t.base0 = w.ctr0;
-      t.base1 = w.ctr1;
-      w.ctr0 += uint32_t(t.grid);
-      w.ctr1 += uint32_t(lsq_reducers(ts.dtype, int(ts.cols)));
       b.block0[k] = blocks;
       blocks += t.grid;
       const double es = dtype == MPA_F64 ? 8.0 : 4.0;
@@ -1234,7 +1224,7 @@ class HipComm final : public Comm {
   std::string tfail_msg_;
 
  public:
-  void init_ticket() { ticket_ = ctr_ + 2 * nworkers_; }
+  void init_ticket() { ticket_ = ctr_ + kLsqCtrPerTask * nworkers_; }
 };
 
 }  // namespace
