@@ -133,12 +133,20 @@ def kernel_name(cfg):
     return "lsq_grad_kernel (one batched launch per epoch per GPU)"
 
 
-def report(args, cfg, world, el, kl, kms, kbytes, extra):
+def report(args, cfg, world, el, per_rank, extra):
+    """per_rank: (launches, summed kernel ms, algorithmic bytes, busy ms) of each GPU.
+    roofline.achieved = algorithmic bytes / busy time (the union of the launch intervals, so
+    concurrent single-task launches of delayed workers are not double counted), averaged
+    over the GPUs; avg_launch_ms = summed kernel ms / launches."""
     its = args.steps / el
     n, rows, cols = cfg["workers"], cfg["rows"], cfg["cols"]
+    kl = sum(p[0] for p in per_rank)
+    kms = sum(p[1] for p in per_rank)
+    kbytes = sum(p[2] for p in per_rank)
+    rates = [p[2] / (p[3] / 1e3) / 1e9 for p in per_rank if p[0] and p[3] > 0]
+    achieved = sum(rates) / len(rates) if rates else None
     per_launch_bytes = kbytes / max(kl, 1)
     per_launch_s = kms / 1e3 / max(kl, 1)
-    achieved = per_launch_bytes / per_launch_s / 1e9 if kl else None
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"lsq_pmc_{cfg['config']}.json")
     if os.path.exists(pmc) and world == 1:
@@ -175,7 +183,7 @@ def report(args, cfg, world, el, kl, kms, kbytes, extra):
                      "traffic": traffic,
                      "kernel": kernel_name(cfg),
                      "alg_bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4),
-                     "launches": kl},
+                     "launches": kl, "busy_ms": round(sum(p[3] for p in per_rank), 3)},
         "epoch_alg_GBps": round(epoch_bytes * its / 1e9, 1),
     }
     out.update(extra)
@@ -261,7 +269,7 @@ def run_single(args, cfg):
     loop(args.steps)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    kl, kms, kbytes = comm.timing()
+    timing = comm.timing()
     comm.set_timing(False)
     fresh = int((pool.repochs == pool.epoch).sum())
     M.waitall_(pool, recv, irecv)
@@ -271,7 +279,7 @@ def run_single(args, cfg):
     if cfg["config"] == "c2":
         extra["loop"] += "; python loop beside it"
     extra["cpu_baseline"] = None if (args.no_cpu_baseline or cfg["config"] != "c2") else cpu_baseline(cfg, args.cpu_seconds)
-    print(json.dumps(report(args, cfg, 1, el, kl, kms, kbytes, extra)), flush=True)
+    print(json.dumps(report(args, cfg, 1, el, [timing], extra)), flush=True)
     comm.shutdown()
     comm.close()
     torch.cuda.synchronize()
@@ -340,19 +348,16 @@ def run_multi(args, cfg, rank, world, local):
         comm.serve()  # timed session, returns at shutdown
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-    kl, kms, kbytes = comm.timing()
+    timing = comm.timing()
     comm.set_timing(False)
     dist.barrier()
     stats = [None] * world
-    dist.all_gather_object(stats, (el, kl, kms, kbytes))
+    dist.all_gather_object(stats, (el, timing))
     if rank == 0:
         el_max = max(s[0] for s in stats)
-        kl = sum(s[1] for s in stats)
-        kms = sum(s[2] for s in stats)
-        kbytes = sum(s[3] for s in stats)
         extra = {"x_norm": float(torch.linalg.norm(x).item()), "build": M.lib().mpa_build_info().decode(),
                  "placement": placement, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None}
-        print(json.dumps(report(args, cfg, world, el_max, kl, kms, kbytes, extra)), flush=True)
+        print(json.dumps(report(args, cfg, world, el_max, [s[1] for s in stats], extra)), flush=True)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()

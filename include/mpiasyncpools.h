@@ -188,9 +188,11 @@ int mpa_comm_pause_servers(mpa_comm* comm);
 /* HIP transport: time every worker-task kernel launch with HIP events on the stream it
  * runs on (enable = 1 / 0).  mpa_comm_timing returns, since its previous call:
  * out[0] launches, out[1] summed kernel milliseconds, out[2] summed algorithmic bytes
- * (A_i + b_i + x + g_i of every task in the launch). */
+ * (A_i + b_i + x + g_i of every task in the launch), out[3] the
+ * milliseconds during which at least one of those launches ran (their union: launches of
+ * delayed workers run concurrently). */
 int mpa_comm_set_timing(mpa_comm* comm, int enable);
-int mpa_comm_timing(mpa_comm* comm, double out[3]);
+int mpa_comm_timing(mpa_comm* comm, double out[4]);
 /* SIM transport only: compute time per task and the virtual clock */
 int mpa_comm_sim_set_compute(mpa_comm* comm, int64_t compute_ns);
 int mpa_comm_sim_advance(mpa_comm* comm, int64_t dt_ns);

@@ -2,6 +2,7 @@
 // library failures into a status code + thread-local message (mpa_last_error).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <new>
 #include <string>
 
@@ -16,11 +17,17 @@ int64_t sim_now(const Comm* c);
 void hip_set_stream(Comm* c, void* s);
 void* hip_get_stream(Comm* c);
 void hip_set_timing(Comm* c, bool on);
-void hip_timing(Comm* c, double out[3]);
+void hip_timing(Comm* c, double out[4]);
 extern int g_lsq_grid;
 Comm* make_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg);
 void hip_serve(Comm* c);
 void hip_pause_servers(Comm* c);
+void hip_set_defer_end(Comm* c, bool on);
+void hip_stage_update(Comm* c, int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x, void* mirror,
+                      bool msg_bf16);
+void hip_set_ahead(Comm* c, int64_t left, int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x,
+                   void* mirror, bool msg_bf16);
+void hip_flush(Comm* c);
 Comm* make_host_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg);
 void host_serve(Comm* c);
 void host_pause_servers(Comm* c);
@@ -294,7 +301,7 @@ int mpa_comm_set_timing(mpa_comm* comm, int enable) {
   });
 }
 
-int mpa_comm_timing(mpa_comm* comm, double out[3]) {
+int mpa_comm_timing(mpa_comm* comm, double out[4]) {
   return guarded([&] {
     mpa::Comm& c = comm_of(comm);
     need_hip(c);
@@ -359,20 +366,63 @@ int mpa_lsq_update(mpa_comm* comm, int dtype, void* x, const void* recvbuf, int6
 
 }  // extern "C"
 namespace {
+bool env_off(const char* name) {
+  const char* e = std::getenv(name);
+  return e && *e == '0';
+}
+
+// The iterate update of a descent loop: x -= eta * sum_i w_i chunk_i (fp32 / fp64 x and
+// chunks); the message sent to the workers is x itself, or its bf16 mirror (batched variant).
+struct DescentUpdate {
+  int dtype;
+  int64_t elems;
+  double eta;
+  void* x;
+  void* mirror;
+  bool msg_bf16;
+};
+
 // The coordinator loop shared by mpa_lsq_descent / mpa_lsqb_descent: `epochs` iterations of
-// asyncmap! followed by the iterate update (examples/iterative_example.jl:37-47).
-template <typename Update>
-int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_bytes, int64_t elems, size_t reply_es,
-                 void* recvbuf, void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
-                 void* nwait_ctx, double stale_weight, int64_t epochs, Update update) {
+// asyncmap! followed by the iterate update (examples/iterative_example.jl:37-47).  The
+// update is staged into the next flush (one fused epoch kernel: harvests + update +
+// dispatch copies + doorbells), and with integer nwait == n the next epoch is enqueued
+// ahead while this one's waits run (HipComm::set_ahead).  MPA_FUSE=0 runs
+// the update as its own launch after every call, MPA_AHEAD=0 disables launch-ahead.
+int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_bytes, size_t reply_es, void* recvbuf,
+                 void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
+                 void* nwait_ctx, double stale_weight, int64_t epochs, const DescentUpdate& up) {
   mpa::Pool& p = pool->p;
   const int64_t n = p.n;
+  const int64_t elems = up.elems;
   const size_t rl = size_t(elems) * reply_es;
+  int rc = guarded([&] {
+    if (!comm || !comm->c) mpa::fail(MPA_ARGUMENT_ERROR, "comm is NULL");
+    need_hip(*comm->c);
+  });
+  if (rc != MPA_OK) return rc;
+  mpa::Comm* c = comm->c;
+  const bool fuse = !env_off("MPA_FUSE");
+  const bool ahead = fuse && !env_off("MPA_AHEAD") && nwait_kind == MPA_NWAIT_INT && nwait == n;
   std::vector<double> w(static_cast<size_t>(n), 0.0);
+  const std::vector<double> w_all(static_cast<size_t>(n), 1.0);  // every chunk fresh
+  struct Restore {
+    mpa::Comm* c;
+    bool on;
+    ~Restore() {
+      if (on) mpa::hip_set_defer_end(c, false);
+    }
+  } restore{c, fuse};
+  if (fuse) mpa::hip_set_defer_end(c, true);
   for (int64_t e = 0; e < epochs; ++e) {
-    int rc = mpa_asyncmap(pool, msg, msg_bytes, recvbuf, size_t(n) * rl, size_t(n * elems), isendbuf,
-                          size_t(n) * msg_bytes, irecvbuf, size_t(n) * rl, comm, nwait_kind, nwait, nwait_fn, nwait_ctx,
-                          "Int64", p.epoch + 1, 0, nullptr);
+    if (ahead) {
+      rc = guarded([&] {
+        mpa::hip_set_ahead(c, epochs - 1 - e, up.dtype, elems, w_all.data(), n, up.eta, up.x, up.mirror, up.msg_bf16);
+      });
+      if (rc != MPA_OK) return rc;
+    }
+    rc = mpa_asyncmap(pool, msg, msg_bytes, recvbuf, size_t(n) * rl, size_t(n * elems), isendbuf, size_t(n) * msg_bytes,
+                      irecvbuf, size_t(n) * rl, comm, nwait_kind, nwait, nwait_fn, nwait_ctx, "Int64", p.epoch + 1, 0,
+                      nullptr);
     if (rc != MPA_OK) return rc;
     double sum = 0;
     for (int64_t i = 0; i < n; ++i) {
@@ -383,10 +433,24 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
     }
     const double s = sum > 0 ? double(n) / sum : 0.0;
     for (auto& v : w) v *= s;
-    rc = update(w.data());
+    if (fuse) {
+      rc = guarded([&] {
+        mpa::hip_stage_update(c, up.dtype, elems, w.data(), n, up.eta, up.x, up.mirror, up.msg_bf16);
+      });
+    } else {
+      rc = aggregate_impl(comm, up.dtype, recvbuf, n, elems, w.data(), up.x, 1, up.eta, up.mirror);
+    }
     if (rc != MPA_OK) return rc;
   }
-  return MPA_OK;
+  if (fuse) {
+    rc = guarded([&] {
+      mpa::hip_set_ahead(c, 0, up.dtype, elems, w_all.data(), n, up.eta, up.x, up.mirror, up.msg_bf16);
+      mpa::hip_set_defer_end(c, false);
+      restore.on = false;
+      mpa::hip_flush(c);  // the last call's harvests and update
+    });
+  }
+  return rc;
 }
 }  // namespace
 extern "C" {
@@ -401,10 +465,8 @@ int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t 
   });
   if (rc != MPA_OK) return rc;
   const size_t es = dtype == MPA_F64 ? 8 : 4;
-  const int64_t n = pool->p.n;
-  return descent_loop(pool, comm, x, size_t(cols) * es, cols, es, recvbuf, isendbuf, irecvbuf, nwait_kind, nwait,
-                      nwait_fn, nwait_ctx, stale_weight, epochs,
-                      [&](const double* w) { return mpa_lsq_update(comm, dtype, x, recvbuf, n, cols, w, eta); });
+  return descent_loop(pool, comm, x, size_t(cols) * es, es, recvbuf, isendbuf, irecvbuf, nwait_kind, nwait, nwait_fn,
+                      nwait_ctx, stale_weight, epochs, DescentUpdate{dtype, cols, eta, x, nullptr, false});
 }
 
 int mpa_nwait_first_plus(void* ctx, int64_t epoch, const int64_t* repochs, int64_t n) {
@@ -430,10 +492,8 @@ int mpa_lsqb_descent(mpa_pool* pool, mpa_comm* comm, void* x32, void* xb16, int6
     if (!x32 || !xb16 || elems <= 0 || epochs < 0) mpa::fail(MPA_ARGUMENT_ERROR, "lsqb_descent: bad arguments");
   });
   if (rc != MPA_OK) return rc;
-  const int64_t n = pool->p.n;
-  return descent_loop(pool, comm, xb16, size_t(elems) * 2, elems, 4, recvbuf, isendbuf, irecvbuf, nwait_kind, nwait,
-                      nwait_fn, nwait_ctx, stale_weight, epochs,
-                      [&](const double* w) { return mpa_lsqb_update(comm, x32, xb16, recvbuf, n, elems, w, eta); });
+  return descent_loop(pool, comm, xb16, size_t(elems) * 2, 4, recvbuf, isendbuf, irecvbuf, nwait_kind, nwait, nwait_fn,
+                      nwait_ctx, stale_weight, epochs, DescentUpdate{MPA_F32, elems, eta, x32, xb16, true});
 }
 
 int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count, double scale,

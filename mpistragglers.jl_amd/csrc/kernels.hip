@@ -114,6 +114,66 @@ __global__ void __launch_bounds__(kThreads) aggregate_kernel(AggregateArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// The fused coordinator epoch step (EpochArgs).  Same arithmetic as aggregate_kernel (fp64
+// sum in chunk order), so the fused and unfused loops produce identical iterates.
+template <typename T>
+__global__ void __launch_bounds__(kThreads) epoch_kernel(EpochArgs a) {
+  T* recv = reinterpret_cast<T*>(a.recv);
+  T* x = static_cast<T*>(a.x);
+  for (int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j < a.elems;
+       j += int64_t(gridDim.x) * blockDim.x) {
+    T v = x[j];
+    if (a.update) {
+      double s = 0.0;
+      for (int i = 0; i < a.n; ++i) {
+        T c;
+        if (a.hsrc[i]) {
+          c = reinterpret_cast<const T*>(a.hsrc[i])[j];
+          recv[int64_t(i) * a.elems + j] = c;
+        } else if (a.w[i] != 0.0) {
+          c = recv[int64_t(i) * a.elems + j];
+        } else {
+          continue;
+        }
+        if (a.w[i] != 0.0) s += a.w[i] * double(c);
+      }
+      v = T(double(v) - a.eta * s);
+      x[j] = v;
+    } else {
+      for (int i = 0; i < a.n; ++i)
+        if (a.hsrc[i]) recv[int64_t(i) * a.elems + j] = reinterpret_cast<const T*>(a.hsrc[i])[j];
+    }
+    for (int i = 0; i < a.n; ++i)
+      if (a.hsrc2[i]) recv[int64_t(i) * a.elems + j] = reinterpret_cast<const T*>(a.hsrc2[i])[j];
+    if (a.msg_bf16) {  // the message is the bf16 mirror (batched variant): a.mirror != NULL
+      const uint16_t h = a.update ? f32_to_bf16_rne(float(v)) : a.mirror[j];
+      if (a.update) a.mirror[j] = h;
+      for (int d = 0; d < a.ndst; ++d) reinterpret_cast<uint16_t*>(a.dst[d])[j] = h;
+    } else {
+      if (a.update && a.mirror) a.mirror[j] = f32_to_bf16_rne(float(v));
+      for (int d = 0; d < a.ndst; ++d) reinterpret_cast<T*>(a.dst[d])[j] = v;
+    }
+  }
+  if (a.ndoor == 0) return;
+  // as exchange_kernel: every block's stores drained and released at system scope, then the
+  // last block to arrive rings the doorbells
+  __shared__ unsigned s_last;
+  drain_vm();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    drain_vm();
+    const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old - a.ticket_base) == gridDim.x - 1;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (int d = 0; d < a.ndoor; ++d)
+        __hip_atomic_store(a.door[d], a.doorval[d], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -174,6 +234,19 @@ hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s) {
   if (grid <= 0) return hipSuccess;
   if (dtype == MPA_F32) hipLaunchKernelGGL(aggregate_kernel<float>, dim3(grid), dim3(kThreads), 0, s, a);
   else if (dtype == MPA_F64) hipLaunchKernelGGL(aggregate_kernel<double>, dim3(grid), dim3(kThreads), 0, s, a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+int epoch_grid(int64_t elems) {
+  const int64_t g = (elems + kThreads - 1) / kThreads;
+  return int(g < 1 ? 1 : g > 1024 ? 1024 : g);
+}
+
+hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s) {
+  const int grid = epoch_grid(a.elems);
+  if (dtype == MPA_F32) hipLaunchKernelGGL(epoch_kernel<float>, dim3(grid), dim3(kThreads), 0, s, a);
+  else if (dtype == MPA_F64) hipLaunchKernelGGL(epoch_kernel<double>, dim3(grid), dim3(kThreads), 0, s, a);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -142,6 +142,39 @@ struct AggregateArgs {
 };
 hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s);
 
+// One coordinator epoch step as ONE launch (the native descent loop): the
+// pending harvest copies `recvbufs[i] .= irecvbufs[i]` of the previous call, the iterate
+// update x -= eta * sum_i w_i chunk_i (the user code between two asyncmap! calls,
+// examples/iterative_example.jl:41-46), the harvests of this call's phase 1, and the
+// dispatch copies `isendbufs[i] .= sendbuf` (:130) of the updated iterate, then the
+// doorbells of remote workers.  Element-parallel: element j of every chunk, of x and of
+// every message is handled by one thread, so the stages need no grid-wide ordering.
+constexpr int kMaxEpochChunks = 16;
+constexpr int kMaxEpochDst = 32;
+struct EpochArgs {
+  int64_t elems;  // elements per chunk (T) = per message
+  int n;          // chunks of recvbuf
+  int update;     // 0: no update stage (the message is x as it stands)
+  uint8_t* recv;  // recvbuf, chunk i at i * elems
+  const uint8_t* hsrc[kMaxEpochChunks];   // harvest source of chunk i before the update (NULL: none)
+  const uint8_t* hsrc2[kMaxEpochChunks];  // harvest source of chunk i after it
+  double w[kMaxEpochChunks];
+  double eta;
+  void* x;           // T[elems], updated in place
+  uint16_t* mirror;  // bf16 copy of the updated x (batched variant) or NULL
+  int msg_bf16;      // the message is the bf16 mirror (else x)
+  int ndst;
+  uint8_t* dst[kMaxEpochDst];
+  int ndoor;
+  unsigned long long* door[kMaxDoorbells];
+  unsigned long long doorval[kMaxDoorbells];
+  uint32_t* ticket;
+  uint32_t ticket_base;
+};
+// grid (blocks) the launch uses: the caller advances the doorbell ticket by it
+int epoch_grid(int64_t elems);
+hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s);
+
 hipError_t launch_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count,
                            double scale, hipStream_t s);
 

@@ -24,6 +24,8 @@
 //   M_DPP       wave reduction by DPP row ops + readlane instead of ds_bpermute
 //   M_PREFETCH  register double buffer: the next tile's loads issue before this tile's math
 //   M_NT        non-temporal loads of A (streamed once)
+//   M_TREE_FENCE  reduction-tree hand-offs by plain stores + agent release / acquire fences
+//               instead of write-through (sc1) stores and loads
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -37,7 +39,7 @@ namespace {
 
 using namespace dev;
 
-enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8 };
+enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16 };
 
 template <typename T>
 struct VecOf;
@@ -110,6 +112,33 @@ __device__ __forceinline__ T wave_sum(T v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
   }
+}
+
+// Slab partials move between workgroups write-through: 8-B relaxed agent-scope stores and
+// loads (global_store/load_dwordx2 sc1: L1 bypassed, L2-served), so a hand-off needs no
+// release / acquire fence (MI355X_MICROARCH.md §inter-workgroup visibility, the "one lane
+// adds for the workgroup, the last adder loads" row): each storing wave drains its stores
+// before the workgroup barrier, one lane then adds to the group counter.
+template <typename T>
+__device__ __forceinline__ void st_sc1(Pack<T>* p, const Pack<T>& v) {
+  struct U2 {
+    unsigned long long a, b;
+  };
+  const U2 u = __builtin_bit_cast(U2, v);
+  unsigned long long* d = reinterpret_cast<unsigned long long*>(p);
+  __hip_atomic_store(d, u.a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(d + 1, u.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ Pack<T> ld_sc1(const Pack<T>* p) {
+  struct U2 {
+    unsigned long long a, b;
+  };
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+  U2 u;
+  u.a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  u.b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_bit_cast(Pack<T>, u);
 }
 
 template <typename T, int VPL, int RB, int MODE>
@@ -249,8 +278,9 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   }
   // Cross-workgroup reduction: a fan-in-8 tree over the workgroup partials, with no
   // waiting.  Level l groups 8 consecutive level-l partials; the member that arrives LAST
-  // at its group's counter (release before the add, acquire after it) sums the group in
-  // member order and carries the result to level l+1; the others return.  A workgroup
+  // at its group's counter sums the group in member order and carries the result to level
+  // l+1; the others return.  Partials are stored and loaded write-through (st_sc1 /
+  // ld_sc1), so the hand-offs need no fences.  A workgroup
   // only ever reads partials whose writers have already arrived, so the tree completes
   // whatever the residency (concurrent launches of delayed workers filled the chip with
   // spinning reducers under the earlier wait-for-all scheme: fp64, 2048 columns, 8
@@ -271,7 +301,16 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   if (G == 1) {
     for (int j = tid; j < S; j += kThreads) store_out(j, red[j]);
   } else {
-    for (int j = tid; j < S; j += kThreads) slab[size_t(blk) * S + j] = red[j];
+    constexpr bool FENCE = (MODE & M_TREE_FENCE) != 0;
+    auto put = [&](P* d, const P& v) {
+      if constexpr (FENCE) *d = v;
+      else st_sc1(d, v);
+    };
+    auto get = [&](const P* q) -> P {
+      if constexpr (FENCE) return *q;
+      else return ld_sc1(q);
+    };
+    for (int j = tid; j < S; j += kThreads) put(&slab[size_t(blk) * S + j], red[j]);
     unsigned idx = unsigned(blk), count = G, stride = 1;
     int lvl_off = 0, lvl_cap = kLsqMaxGrid / int(F);
     for (;;) {
@@ -281,14 +320,18 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       const unsigned gsize = count - first < F ? count - first : F;
       if (tid == 0) {
         unsigned* c = &a.ctr[lvl_off + int(idx / F)];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        drain_vm();
+        if constexpr (FENCE) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          drain_vm();
+        }
         const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_ticket = old + 1 == gsize;
         if (s_ticket) {
           __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          drain_vm();
+          if constexpr (FENCE) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            drain_vm();
+          }
         }
       }
       __syncthreads();
@@ -299,7 +342,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
         P t[F];
 #pragma unroll
         for (unsigned m = 0; m < F; ++m)
-          if (m < gsize) t[m] = src[size_t(m) * stride * S + j];
+          if (m < gsize) t[m] = get(&src[size_t(m) * stride * S + j]);
         P s = t[0];
 #pragma unroll
         for (unsigned m = 1; m < F; ++m)
@@ -307,7 +350,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
 #pragma unroll
             for (int e = 0; e < E; ++e) s.v[e] += t[m].v[e];
         if (next == 1) store_out(j, s);
-        else slab[size_t(first) * stride * S + j] = s;
+        else put(&slab[size_t(first) * stride * S + j], s);
       }
       if (next == 1) break;
       idx /= F;
@@ -354,6 +397,7 @@ constexpr Variant kC2Variants[] = {
     {go<float, 4, 2, M_CLAMP | M_DPP | M_PREFETCH | M_NT>, 2, "rb2+clamp+dpp+prefetch+nt"},
     {go<float, 4, 8, M_CLAMP | M_DPP>, 8, "rb8+clamp+dpp"},
     {go<float, 4, 2, M_CLAMP | M_DPP>, 2, "rb2+clamp+dpp"},
+    {go<float, 4, 4, M_CLAMP | M_DPP | M_NT | M_TREE_FENCE>, 4, "rb4+clamp+dpp+nt+fenced-tree"},
 };
 constexpr int kNumC2Variants = int(sizeof(kC2Variants) / sizeof(kC2Variants[0]));
 constexpr int kDefaultC2 = 5;  // rb4+clamp+dpp+nt: 6.5 TB/s on c2 (profiles/r01_tune.txt)

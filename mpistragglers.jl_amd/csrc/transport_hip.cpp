@@ -143,6 +143,8 @@ struct HipWorker {
   // go_dev = device copy of the doorbell it ran on; counter bases to restore if cancelled
   bool armed = false;
   unsigned long long* go_dev = nullptr;
+  // coordinator, launch-ahead: the next post / harvest of this worker is already enqueued
+  bool preposted = false, preharvest = false;
   uint32_t arm_sbase = 0, arm_tbase = 0;
 };
 
@@ -307,12 +309,24 @@ class HipComm final : public Comm {
   void begin_call(const CallBufs& b) override {
     if (role_ == SERVER) fail(MPA_ERROR, "asyncmap!/waitall! run on rank 0; this process serves workers (mpa_comm_serve)");
     b_ = b;
+    call_posts_.clear();
   }
 
   void post(int64_t i, int64_t rank, int64_t tag) override {
     (void)tag;
     if (shutdown_) fail(MPA_ERROR, "comm has been shut down");
     HipWorker& w = w_[size_t(rank - 1)];
+    call_posts_.push_back({i, rank});
+    if (w.preposted) {
+      // enqueued one epoch ahead (enqueue_ahead): same slot and buffers, nothing to launch
+      if (w.slot != i || w.sl != b_.sl || w.rl != b_.rl || b_.isendbuf != ahead_bufs_.isendbuf ||
+          b_.irecvbuf != ahead_bufs_.irecvbuf || b_.recvbuf != ahead_bufs_.recvbuf || b_.sendbuf != ahead_bufs_.sendbuf)
+        fail(MPA_ERROR, "launch-ahead: the call posts worker %lld differently from the epoch enqueued ahead",
+             (long long)rank);
+      w.preposted = false;
+      w.seq += 1;
+      return;
+    }
     if (w.remote) {
       if (b_.sl > region_->max_msg() || b_.rl > region_->max_msg())
         fail(MPA_DIMENSION_MISMATCH, "messages of %zu / %zu bytes exceed the communicator's mailbox of %zu bytes",
@@ -331,7 +345,14 @@ class HipComm final : public Comm {
     posts_.push_back(rank);
   }
 
-  void harvest(int64_t i, int64_t rank) override { harv_.push_back({i, rank}); }
+  void harvest(int64_t i, int64_t rank) override {
+    HipWorker& w = w_[size_t(rank - 1)];
+    if (w.preharvest) {  // already in the epoch kernel enqueued ahead
+      w.preharvest = false;
+      return;
+    }
+    harv_.push_back({i, rank});
+  }
 
   bool test(int64_t i, int64_t rank) override {
     (void)i;
@@ -363,45 +384,82 @@ class HipComm final : public Comm {
   }
 
   void flush() override {
-    if (posts_.empty() && harv_.empty()) return;
+    if (posts_.empty() && harv_.empty() && !has_update_) {
+      maybe_ahead();
+      return;
+    }
     if (timing_) reap_timing(false);
-    ExchangeBuilder xb(ticket_, &ticket_count_, coord_);
-    // harvests first: a worker re-posted by this flush is only told to go (doorbell, or
-    // the event below) after its previous reply has been copied out
-    for (const auto& h : harv_) {
-      const HipWorker& w = w_[size_t(h.rank - 1)];
-      const uint8_t* src = w.remote ? w.box_reply_dev : b_.irecvbuf + size_t(h.slot) * b_.rl;
-      xb.copy(src, b_.recvbuf + size_t(h.slot) * b_.rl, b_.rl);
-    }
-    bool local_posts = false;
-    for (int64_t rank : posts_) {
-      const HipWorker& w = w_[size_t(rank - 1)];
-      uint8_t* slot = b_.isendbuf + size_t(w.slot) * b_.sl;
-      if (w.remote) {
-        xb.reserve(2, 1);
-        xb.copy(b_.sendbuf, slot, b_.sl);
-        xb.copy(b_.sendbuf, w.box_msg_dev, b_.sl);
-        xb.door(w.box_door_dev, w.seq);
-      } else {
-        xb.copy(b_.sendbuf, slot, b_.sl);
-        local_posts = true;
+    if (has_update_ && fused_ok(upd_, posts_)) {
+      emit_epoch(harv_, harv_before_, posts_, upd_, coord_);
+    } else {
+      ExchangeBuilder xb(ticket_, &ticket_count_, coord_);
+      size_t h0 = 0;
+      if (has_update_) {  // unfused: harvests before the update, the update, then the rest
+        for (; h0 < harv_before_; ++h0) add_harvest(xb, harv_[h0]);
+        xb.launch();
+        launch_update(upd_);
       }
+      for (size_t k = h0; k < harv_.size(); ++k) add_harvest(xb, harv_[k]);
+      for (int64_t rank : posts_) {
+        const HipWorker& w = w_[size_t(rank - 1)];
+        uint8_t* slot = b_.isendbuf + size_t(w.slot) * b_.sl;
+        if (w.remote) {
+          xb.reserve(2, 1);
+          xb.copy(b_.sendbuf, slot, b_.sl);
+          xb.copy(b_.sendbuf, w.box_msg_dev, b_.sl);
+          xb.door(w.box_door_dev, w.seq);
+        } else {
+          xb.copy(b_.sendbuf, slot, b_.sl);
+        }
+      }
+      xb.launch();
     }
-    xb.launch();
+    has_update_ = false;
     harv_.clear();
-    if (local_posts) {
-      std::vector<int64_t> here;
-      for (int64_t rank : posts_)
-        if (!w_[size_t(rank - 1)].remote) here.push_back(rank);
-      // every task of this call is awaited before the caller enqueues anything else on the
-      // coordinator stream: run the batch right behind the exchange on that stream (a
-      // cross-queue event wait costs ~35 us per epoch, profiles/r01_c2_gaps.json)
-      launch_tasks(here, /*staged=*/false, /*on_coord=*/b_.await_all);
-    }
+    launch_local(posts_);
     posts_.clear();
+    maybe_ahead();
   }
 
-  void end_call() override { flush(); }
+  void end_call() override {
+    if (!defer_end_) flush();
+  }
+
+  // ---- the native descent loop (capi.cpp descent_loop) ----
+  // The iterate update between two asyncmap! calls, folded into the next flush (one epoch
+  // kernel: harvests, update, dispatch copies, doorbells) instead of its own launches.
+  struct UpdateSpec {
+    int dtype = MPA_F32;  // of x and of the recv chunks
+    int64_t elems = 0;
+    std::vector<double> w;
+    double eta = 0;
+    void* x = nullptr;
+    uint16_t* mirror = nullptr;  // bf16 copy of x; the message when msg_bf16
+    bool msg_bf16 = false;
+  };
+  // end_call() leaves the call's harvests pending (they join the next flush's epoch kernel)
+  void set_defer_end_flush(bool on) { defer_end_ = on; }
+  void stage_update(const UpdateSpec& u) {
+    if (ahead_update_) {  // enqueued ahead with the predicted weights: they must match
+      ahead_update_ = false;
+      if (u.w != ahead_upd_.w || u.x != ahead_upd_.x || u.eta != ahead_upd_.eta || u.elems != ahead_upd_.elems)
+        fail(MPA_ERROR, "launch-ahead: the iterate update differs from the one enqueued ahead");
+      return;
+    }
+    if (has_update_) flush();
+    upd_ = u;
+    has_update_ = true;
+    harv_before_ = harv_.size();
+  }
+  // Launch-ahead (integer nwait == n): the call returns only once all n tasks it posts have
+  // completed fresh, so the next epoch is fully determined before this call's waits begin:
+  // harvest all n, update with weight 1 each, re-post all n.  The phase-2 flush of such a
+  // call enqueues that next epoch (epoch kernel + tasks) right behind this one; the next
+  // call then finds its posts already enqueued.  `epochs_left` = calls still to come.
+  void set_ahead(int64_t epochs_left, const UpdateSpec& pred) {
+    ahead_left_ = epochs_left;
+    ahead_pred_ = pred;
+  }
 
   uint64_t now_ns() override {
     return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count());
@@ -598,6 +656,131 @@ class HipComm final : public Comm {
   struct Harvest {
     int64_t slot, rank;
   };
+
+  void add_harvest(ExchangeBuilder& xb, const Harvest& h) {
+    const HipWorker& w = w_[size_t(h.rank - 1)];
+    const uint8_t* src = w.remote ? w.box_reply_dev : b_.irecvbuf + size_t(h.slot) * b_.rl;
+    xb.copy(src, b_.recvbuf + size_t(h.slot) * b_.rl, b_.rl);
+  }
+
+  // tasks of the workers served here among `posted`, behind the exchange / epoch kernel
+  void launch_local(const std::vector<int64_t>& posted) {
+    std::vector<int64_t> here;
+    for (int64_t rank : posted)
+      if (!w_[size_t(rank - 1)].remote) here.push_back(rank);
+    // every task of this call is awaited before the caller enqueues anything else on the
+    // coordinator stream: run the batch right behind the exchange on that stream (a
+    // cross-queue event wait costs ~35 us per epoch, profiles/r01_c2_gaps.json)
+    if (!here.empty()) launch_tasks(here, /*staged=*/false, /*on_coord=*/b_.await_all);
+  }
+
+  // the update as its own launch (the unfused path)
+  void launch_update(const UpdateSpec& u) {
+    AggregateArgs a{};
+    if (b_.n > kMaxAggregate) fail(MPA_ARGUMENT_ERROR, "aggregate: 0 <= nchunks <= %d", kMaxAggregate);
+    a.chunks = b_.recvbuf;
+    a.out = u.x;
+    a.n = b_.n;
+    a.elems = u.elems;
+    a.stride = u.elems;
+    a.eta = u.eta;
+    a.update = 1;
+    a.mirror = u.mirror;
+    for (int64_t i = 0; i < b_.n; ++i) a.w[i] = u.w[size_t(i)];
+    HIPCHECK(launch_aggregate(u.dtype, a, coord_));
+  }
+
+  bool fused_ok(const UpdateSpec& u, const std::vector<int64_t>& posted) const {
+    const size_t es = u.dtype == MPA_F64 ? 8 : 4;
+    if (b_.n > kMaxEpochChunks || int64_t(u.w.size()) != b_.n || b_.rl != size_t(u.elems) * es ||
+        b_.sl != size_t(u.elems) * (u.msg_bf16 ? 2 : es) || b_.sendbuf != (u.msg_bf16 ? (const uint8_t*)u.mirror : (const uint8_t*)u.x))
+      return false;
+    size_t ndst = 0, ndoor = 0;
+    for (int64_t rank : posted) {
+      const bool remote = w_[size_t(rank - 1)].remote;
+      ndst += remote ? 2 : 1;
+      ndoor += remote ? 1 : 0;
+    }
+    return ndst <= size_t(kMaxEpochDst) && ndoor <= size_t(kMaxDoorbells);
+  }
+
+  // ONE epoch kernel: harvests [0, before) of `hv`, the update, harvests [before, end), the
+  // dispatch copies of the posts (isendbuf slot; mailbox + doorbell for a remote worker)
+  void emit_epoch(const std::vector<Harvest>& hv, size_t before, const std::vector<int64_t>& posted,
+                  const UpdateSpec& u, hipStream_t s) {
+    EpochArgs a{};
+    a.elems = u.elems;
+    a.n = int(b_.n);
+    a.update = 1;
+    a.recv = b_.recvbuf;
+    for (size_t k = 0; k < hv.size(); ++k) {
+      const HipWorker& w = w_[size_t(hv[k].rank - 1)];
+      const uint8_t* src = w.remote ? w.box_reply_dev : b_.irecvbuf + size_t(hv[k].slot) * b_.rl;
+      (k < before ? a.hsrc : a.hsrc2)[hv[k].slot] = src;
+    }
+    for (int64_t i = 0; i < b_.n; ++i) a.w[i] = u.w[size_t(i)];
+    a.eta = u.eta;
+    a.x = u.x;
+    a.mirror = u.mirror;
+    a.msg_bf16 = u.msg_bf16 ? 1 : 0;
+    for (int64_t rank : posted) {
+      const HipWorker& w = w_[size_t(rank - 1)];
+      a.dst[a.ndst++] = b_.isendbuf + size_t(w.slot) * b_.sl;
+      if (w.remote) {
+        a.dst[a.ndst++] = w.box_msg_dev;
+        a.door[a.ndoor] = w.box_door_dev;
+        a.doorval[a.ndoor++] = w.seq;
+      }
+    }
+    if (a.ndoor > 0) {
+      a.ticket = ticket_;
+      a.ticket_base = ticket_count_;
+      ticket_count_ += uint32_t(epoch_grid(a.elems));
+    }
+    HIPCHECK(launch_epoch(u.dtype, a, s));
+  }
+
+  // enqueue the next epoch of an await-all call (set_ahead), once per call, when this
+  // call has posted every worker of the pool
+  void maybe_ahead() {
+    if (ahead_left_ <= 0 || !b_.await_all || int64_t(call_posts_.size()) != b_.n) return;
+    UpdateSpec& u = ahead_pred_;
+    for (const auto& cp : call_posts_)
+      if (w_[size_t(cp.rank - 1)].preposted) return;
+    // the next epoch's posts equal this call's: same slots, same buffers; only workers
+    // whose task starts as soon as its message lands (no injected delay, whose sleep
+    // begins at delivery on the host timer)
+    std::vector<int64_t> posted;
+    for (const auto& cp : call_posts_) {
+      const HipWorker& w = w_[size_t(cp.rank - 1)];
+      const TaskSpec& ts = tasks_[size_t(cp.rank - 1)];
+      if (!w.remote && ((ts.kind != MPA_TASK_LSQ && ts.kind != MPA_TASK_LSQ_BATCH) || !ts.delays_ns.empty())) return;
+      posted.push_back(cp.rank);
+    }
+    if (!fused_ok(u, posted)) return;
+    ahead_left_ = 0;
+    // the replies of this call's remote tasks must have landed before the epoch kernel
+    // reads them (local tasks are stream-ordered before it on the coordinator stream)
+    std::vector<Harvest> hv;
+    for (const auto& cp : call_posts_) {
+      HipWorker& w = w_[size_t(cp.rank - 1)];
+      if (w.remote)
+        HIPCHECK(hipStreamWaitValue64(coord_, region_->dev(&w.box->done), w.seq, hipStreamWaitValueGte, ~0ull));
+      hv.push_back({cp.slot, cp.rank});
+    }
+    for (int64_t rank : posted) w_[size_t(rank - 1)].seq += 1;  // the ahead epoch's task numbers
+    emit_epoch(hv, hv.size(), posted, u, coord_);
+    launch_local(posted);
+    for (int64_t rank : posted) {
+      HipWorker& w = w_[size_t(rank - 1)];
+      w.seq -= 1;  // the pool's view: its next post() takes the enqueued number
+      w.preposted = true;
+      w.preharvest = true;
+    }
+    ahead_bufs_ = b_;
+    ahead_upd_ = u;
+    ahead_update_ = true;
+  }
 
   bool done(int64_t rank) const {
     const HipWorker& w = w_[size_t(rank - 1)];
@@ -1121,15 +1304,29 @@ class HipComm final : public Comm {
     if (!on) reap_timing(true);
     timing_ = on;
   }
-  // launches, total kernel ms, total algorithmic bytes since the last call
-  void timing(double out[3]) {
+  // launches, total kernel ms, total algorithmic bytes, and the ms during which at least
+  // one timed launch was running (the union of their intervals: concurrent single-task
+  // launches of delayed workers overlap) since the last call
+  void timing(double out[4]) {
     reap_timing(true);
+    std::sort(t_iv_.begin(), t_iv_.end());
+    double busy = 0, hi = -1e300;
+    for (const auto& iv : t_iv_) {
+      if (iv.second <= hi) continue;
+      busy += iv.second - (iv.first > hi ? iv.first : hi);
+      hi = iv.second;
+    }
     out[0] = double(t_launches_);
     out[1] = t_ms_;
     out[2] = t_bytes_;
+    out[3] = busy;
     t_launches_ = 0;
     t_ms_ = 0;
     t_bytes_ = 0;
+    t_iv_.clear();
+    std::lock_guard<std::mutex> lk(tm_mu_);
+    if (anchor_) event_pool_.push_back(anchor_);
+    anchor_ = nullptr;
   }
 
  private:
@@ -1172,14 +1369,22 @@ class HipComm final : public Comm {
         timed_[keep++] = tl;
         continue;
       }
+      bool keep_start = false;
       if (!tl.void_) {
-        float ms = 0;
+        float ms = 0, s0 = 0;
         HIPCHECK(hipEventElapsedTime(&ms, tl.start, tl.stop));
+        if (!anchor_) {
+          anchor_ = tl.start;  // interval origin of this timing window
+          keep_start = true;
+        } else {
+          HIPCHECK(hipEventElapsedTime(&s0, anchor_, tl.start));
+        }
+        t_iv_.emplace_back(double(s0), double(s0) + double(ms));
         t_ms_ += ms;
         t_bytes_ += tl.bytes;
         t_launches_ += 1;
       }
-      event_pool_.push_back(tl.start);
+      if (!keep_start) event_pool_.push_back(tl.start);
       event_pool_.push_back(tl.stop);
     }
     timed_.resize(keep);
@@ -1203,6 +1408,15 @@ class HipComm final : public Comm {
   std::vector<int64_t> posts_;
   std::vector<Harvest> harv_;
   CallBufs b_;
+  std::vector<Harvest> call_posts_;  // (slot, rank) of every post() of the current call
+  bool defer_end_ = false;
+  bool has_update_ = false;
+  size_t harv_before_ = 0;  // harvests staged before the pending update
+  UpdateSpec upd_;
+  int64_t ahead_left_ = 0;
+  UpdateSpec ahead_pred_, ahead_upd_;
+  CallBufs ahead_bufs_;
+  bool ahead_update_ = false;
   bool timing_ = false;
   bool debug_ = false;
   int arm_mode_ = 2;
@@ -1210,6 +1424,8 @@ class HipComm final : public Comm {
   std::vector<hipEvent_t> event_pool_;
   int64_t t_launches_ = 0;
   double t_ms_ = 0, t_bytes_ = 0;
+  std::vector<std::pair<double, double>> t_iv_;  // launch intervals (ms from anchor_)
+  hipEvent_t anchor_ = nullptr;
   std::vector<hipStream_t> launch_streams_;
   size_t next_launch_ = 0;
   std::mutex tm_mu_;  // timed_ / event_pool_ (the timer thread also launches)
@@ -1251,8 +1467,34 @@ Comm* make_dist_comm(int64_t nworkers, const int* placement, int my_rank, const 
 void hip_set_stream(Comm* c, void* s) { static_cast<HipComm*>(c)->set_stream(static_cast<hipStream_t>(s)); }
 void* hip_get_stream(Comm* c) { return static_cast<HipComm*>(c)->stream(); }
 void hip_set_timing(Comm* c, bool on) { static_cast<HipComm*>(c)->set_timing(on); }
-void hip_timing(Comm* c, double out[3]) { static_cast<HipComm*>(c)->timing(out); }
+void hip_timing(Comm* c, double out[4]) { static_cast<HipComm*>(c)->timing(out); }
 void hip_serve(Comm* c) { static_cast<HipComm*>(c)->serve(); }
+
+namespace {
+HipComm::UpdateSpec update_spec(int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x,
+                                void* mirror, bool msg_bf16) {
+  HipComm::UpdateSpec u;
+  u.dtype = dtype;
+  u.elems = elems;
+  u.w.assign(w, w + n);
+  u.eta = eta;
+  u.x = x;
+  u.mirror = static_cast<uint16_t*>(mirror);
+  u.msg_bf16 = msg_bf16;
+  return u;
+}
+}  // namespace
+
+void hip_set_defer_end(Comm* c, bool on) { static_cast<HipComm*>(c)->set_defer_end_flush(on); }
+void hip_stage_update(Comm* c, int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x, void* mirror,
+                      bool msg_bf16) {
+  static_cast<HipComm*>(c)->stage_update(update_spec(dtype, elems, w, n, eta, x, mirror, msg_bf16));
+}
+void hip_set_ahead(Comm* c, int64_t left, int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x,
+                   void* mirror, bool msg_bf16) {
+  static_cast<HipComm*>(c)->set_ahead(left, update_spec(dtype, elems, w, n, eta, x, mirror, msg_bf16));
+}
+void hip_flush(Comm* c) { static_cast<HipComm*>(c)->flush(); }
 void hip_pause_servers(Comm* c) { static_cast<HipComm*>(c)->pause_servers(); }
 
 }  // namespace mpa

@@ -141,10 +141,11 @@ class DeviceComm(_Comm):
         check(lib().mpa_comm_set_timing(self._h, 1 if enable else 0))
 
     def timing(self):
-        """(launches, kernel_ms, algorithmic_bytes) since the previous call."""
-        out = (C.c_double * 3)()
+        """(launches, kernel_ms, algorithmic_bytes, busy_ms) since the previous call;
+        busy_ms = the union of the launch intervals (concurrent launches overlap)."""
+        out = (C.c_double * 4)()
         check(lib().mpa_comm_timing(self._h, out))
-        return int(out[0]), float(out[1]), float(out[2])
+        return int(out[0]), float(out[1]), float(out[2]), float(out[3])
 
     def aggregate(self, recvbuf, nchunks, weights, out):
         """out = sum_i weights[i] * chunk_i of recvbuf (device kernel, fixed order)."""

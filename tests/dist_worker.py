@@ -315,3 +315,86 @@ def lsqb_dist(rank, world, port, placement, result_q):
     except Exception:
         result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
         raise
+
+
+def lsq_descent_dist(rank, world, port, placement, env, result_q):
+    """The native descent loop (fused epoch kernel; launch-ahead at nwait = n: the next
+    epoch's doorbells queued behind stream waits on the remote completion words) with
+    workers on several processes, against the same loop run by Python in one process on
+    the same shards: identical iterates, bitwise."""
+    import numpy as np
+    try:
+        os.environ.update(env)
+        dist = _init(rank, world, port)
+        import torch
+        torch.cuda.set_device(0)
+        import mpiasyncpools as M
+        n, rows, cols, seed, epochs, eta = len(placement), 2048, 1024, 23, 7, 0.02
+        name = [f"/mpa_d{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+        if rank == 0:
+            comm = M.DistComm(n, placement, 0, name[0], cols * 4, transport="hip")
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            comm = M.DistComm(n, placement, rank, name[0], cols * 4, transport="hip")
+
+        def shard(w):
+            A = torch.empty(rows, cols, device="cuda")
+            b = torch.empty(rows, device="cuda")
+            M.generate(A, seed, 0, (w - 1) * rows * cols, float(np.float32(1 / np.sqrt(cols))))
+            M.generate(b, seed, 1, (w - 1) * rows, 1.0)
+            return A, b
+
+        keep = []
+        for w in range(1, n + 1):
+            if placement[w - 1] == rank:
+                keep.append(shard(w))
+                comm.set_task_lsq(w, *keep[-1])
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank != 0:
+            comm.serve()
+            dist.barrier()
+            comm.close()
+            dist.destroy_process_group()
+            return
+        pool = M.MPIAsyncPool(n)
+        x = torch.zeros(cols, device="cuda")
+        isend = torch.zeros(n * cols, device="cuda")
+        recv = torch.zeros(n * cols, device="cuda")
+        irecv = torch.zeros_like(recv)
+        M.lsq_descent(pool, comm, x, recv, isend, irecv, n, eta, epochs)
+        torch.cuda.synchronize()
+        errors = []
+        if pool.epoch != epochs or list(pool.repochs) != [epochs] * n or any(pool.active):
+            errors.append(("state", pool.epoch, list(pool.repochs), list(pool.active)))
+        # isendbuf holds the message of the last epoch; recvbuf its harvested replies
+        got_isend = isend.clone()
+        comm.shutdown()
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        # the same loop in one process, Python side (asyncmap_ + lsq_update)
+        lc = M.DeviceComm(n)
+        shards = [shard(w) for w in range(1, n + 1)]
+        for w in range(1, n + 1):
+            lc.set_task_lsq(w, *shards[w - 1])
+        lp = M.MPIAsyncPool(n)
+        x2 = torch.zeros(cols, device="cuda")
+        isend2 = torch.zeros(n * cols, device="cuda")
+        recv2 = torch.zeros(n * cols, device="cuda")
+        irecv2 = torch.zeros_like(recv2)
+        for _ in range(epochs):
+            rep = M.asyncmap_(lp, x2, recv2, isend2, irecv2, lc, nwait=n)
+            lc.lsq_update(x2, recv2, n, (rep == lp.epoch) * 1.0, eta)
+        torch.cuda.synchronize()
+        if not torch.equal(x.view(torch.int32), x2.view(torch.int32)):
+            errors.append(("x", float((x - x2).abs().max())))
+        if not torch.equal(recv.view(torch.int32), recv2.view(torch.int32)):
+            errors.append(("recvbuf", float((recv - recv2).abs().max())))
+        if not torch.equal(got_isend.view(torch.int32), isend2.view(torch.int32)):
+            errors.append(("isendbuf",))
+        lc.close()
+        result_q.put(("ok", errors))
+    except Exception:
+        result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
+        raise

@@ -335,11 +335,15 @@ def test_full_size_c2_against_torch_fp64(M, torch_mod):
     assert torch.equal(isend.view(n, cols), x.expand(n, cols))
 
 
-def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod):
+@pytest.mark.parametrize("env", [{}, {"MPA_AHEAD": "0"}, {"MPA_FUSE": "0"}])
+def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod, monkeypatch, env):
     """mpa_lsq_descent makes the same calls as the Python loop: identical iterates (bitwise,
-    nwait = n so every epoch is fresh and every kernel is deterministic)."""
+    nwait = n so every epoch is fresh and every kernel is deterministic), with the fused
+    epoch kernel and launch-ahead (default), fused only, and unfused."""
     import lsq
     torch = torch_mod
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     n, rows, cols, seed = 4, 2048, 1024, 17
     A = _dev(torch, lsq.gen_matrix(seed, 0, n * rows, cols, "f32"))
     b = _dev(torch, lsq.gen_vector(seed, 0, n * rows, "f32"))
@@ -361,7 +365,10 @@ def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod):
                 comm.lsq_update(x, recv, n, (rep == pool.epoch) * 1.0, 0.01)
         torch.cuda.synchronize()
         assert pool.epoch == 6
-        xs.append(x.clone())
+        assert list(pool.repochs) == [6] * n and not any(pool.active)
+        xs.append((x.clone(), recv.clone(), isend.clone()))
         comm.close()
-    assert torch.equal(xs[0].view(torch.int32), xs[1].view(torch.int32))
+    for a, b in zip(xs[0], xs[1]):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    xs = [xs[0][0], xs[1][0]]
     assert float(torch.linalg.norm(xs[0])) > 0

@@ -58,3 +58,16 @@ def test_lsqb_two_processes_prearmed(built):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run(dist_worker.lsqb_dist, 2, [0, 1])
+
+
+@pytest.mark.parametrize("placement,env", [
+    ([0, 1, 1, 1], {}),                                   # rank 1 serves 3 workers (host-launched)
+    ([0, 1], {}),                                         # one worker per process: pre-armed
+    ([0, 1, 1], {"MPA_AHEAD": "0"}),                      # fused epoch kernel, no launch-ahead
+    ([0, 1], {"MPA_FUSE": "0"}),                          # the unfused loop
+])
+def test_lsq_descent_two_processes(built, placement, env):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.lsq_descent_dist, 2, placement, env)

@@ -158,3 +158,36 @@ def test_lsqb_full_c5_shard_against_torch_fp64(M):
         assert err <= TOL, (i, err)
         del Ai, G
     comm.close()
+
+
+@pytest.mark.parametrize("env", [{}, {"MPA_AHEAD": "0"}, {"MPA_FUSE": "0"}])
+def test_lsqb_descent_native_loop_matches_python_loop(M, monkeypatch, env):
+    """mpa_lsqb_descent (fused epoch kernel: harvests, fp32 update, bf16 mirror, dispatch
+    of the mirror; launch-ahead at nwait = n) against the Python loop (asyncmap_ +
+    lsqb_update): identical fp32 iterates, bf16 messages and replies, bitwise."""
+    import torch
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n, rows, cols, epochs, eta = 3, 600, 256, 5, 0.01
+    A, B, _ = _problem(n * rows, cols, seed=13)
+    outs = []
+    for native in (False, True):
+        comm = M.DeviceComm(n)
+        for r in range(1, n + 1):
+            comm.set_task_lsq_batch(r, _bf16(torch, A[(r - 1) * rows:r * rows]), _bf16(torch, B[(r - 1) * rows:r * rows]))
+        pool = M.MPIAsyncPool(n)
+        bufs = _Bufs(torch, n, cols)
+        x32 = torch.zeros(cols * K, device="cuda")
+        if native:
+            M.lsqb_descent(pool, comm, x32, bufs.send, bufs.recv, bufs.isend, bufs.irecv, n, eta, epochs)
+        else:
+            for _ in range(epochs):
+                rep = M.asyncmap_(pool, bufs.send, bufs.recv, bufs.isend, bufs.irecv, comm, nwait=n)
+                comm.lsqb_update(x32, bufs.send, bufs.recv, n, (rep == pool.epoch) * 1.0, eta)
+        torch.cuda.synchronize()
+        assert pool.epoch == epochs and list(pool.repochs) == [epochs] * n
+        outs.append((x32.clone(), bufs.send.clone().view(torch.int16), bufs.recv.clone(), bufs.isend.clone().view(torch.int16)))
+        comm.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a.view(torch.int16) if a.dtype != torch.int16 else a, b.view(torch.int16) if b.dtype != torch.int16 else b)
+    assert float(torch.linalg.norm(outs[0][0])) > 0

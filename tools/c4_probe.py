@@ -40,7 +40,7 @@ def run(label, nw, delays):
         M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=nw)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / 3
-    kl, kms, kb = comm.timing()
+    kl, kms, kb, _ = comm.timing()
     print("%-28s %8.3f ms/epoch  %d launches  %.3f ms/launch  %.1f GB/s/launch  %.1f GB/s epoch" %
           (label, el * 1e3, kl, kms / max(kl, 1), kb / max(kl, 1) / (kms / max(kl, 1)) / 1e6, kb / 3 / el / 1e9), flush=True)
     comm.shutdown()

@@ -89,7 +89,7 @@ def main():
                     M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=n)
                 torch.cuda.synchronize()
                 el = time.perf_counter() - t0
-                launches, ms, by = comm.timing()
+                launches, ms, by, _ = comm.timing()
                 comm.set_timing(False)
                 print(json.dumps({"round": rnd, "variant": v,
                                   "grid": g, "kernel_GBps": round(by / (ms / 1e3) / 1e9, 1),
