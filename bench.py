@@ -355,8 +355,9 @@ def run_multi(args, cfg, rank, world, local):
     dist.all_gather_object(stats, (el, timing))
     if rank == 0:
         el_max = max(s[0] for s in stats)
+        paths = sorted({comm.payload_path(w) for w in range(1, n + 1) if placement[w - 1] != 0} - {None})
         extra = {"x_norm": float(torch.linalg.norm(x).item()), "build": M.lib().mpa_build_info().decode(),
-                 "placement": placement, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None}
+                 "placement": placement, "payload_path": "/".join(paths) or None, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None}
         print(json.dumps(report(args, cfg, world, el_max, [s[1] for s in stats], extra)), flush=True)
     dist.barrier()
     comm.close()

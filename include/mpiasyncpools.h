@@ -185,6 +185,10 @@ int mpa_comm_create_dist(int transport, int64_t nworkers, const int* placement, 
 int mpa_comm_serve(mpa_comm* comm);
 /* rank 0: make every running mpa_comm_serve return (e.g. around a barrier) */
 int mpa_comm_pause_servers(mpa_comm* comm);
+/* rank 0 of a HIP multi-process communicator: the payload path of worker `rank` once its
+ * first message was posted: 0 not yet decided / not a remote worker, 1 host shared-memory
+ * mailbox, 2 device memory over xGMI (HIP IPC; MPA_XGMI=0 forces 1) */
+int mpa_comm_payload_path(mpa_comm* comm, int64_t rank);
 /* HIP transport: time every worker-task kernel launch with HIP events on the stream it
  * runs on (enable = 1 / 0).  mpa_comm_timing returns, since its previous call:
  * out[0] launches, out[1] summed kernel milliseconds, out[2] summed algorithmic bytes

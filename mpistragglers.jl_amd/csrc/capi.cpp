@@ -28,6 +28,7 @@ void hip_stage_update(Comm* c, int dtype, int64_t elems, const double* w, int64_
 void hip_set_ahead(Comm* c, int64_t left, int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x,
                    void* mirror, bool msg_bf16);
 void hip_flush(Comm* c);
+int hip_payload_path(Comm* c, int64_t rank);
 Comm* make_host_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg);
 void host_serve(Comm* c);
 void host_pause_servers(Comm* c);
@@ -173,6 +174,11 @@ int mpa_comm_serve(mpa_comm* comm) {
     else if (c.transport() == MPA_TRANSPORT_HOST) mpa::host_serve(&c);
     else mpa::fail(MPA_ARGUMENT_ERROR, "not a multi-process communicator");
   });
+}
+
+int mpa_comm_payload_path(mpa_comm* comm, int64_t rank) {
+  if (!comm || !comm->c || comm->c->transport() != MPA_TRANSPORT_HIP) return 0;
+  return mpa::hip_payload_path(comm->c, rank);
 }
 
 int mpa_comm_pause_servers(mpa_comm* comm) {

@@ -34,9 +34,11 @@ __device__ __forceinline__ void publish_done(unsigned long long* flag, unsigned 
   __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// A pre-armed launch whose doorbell was rung with kCancelBit: return before any work.
-__device__ __forceinline__ bool disarmed(const unsigned long long* go) {
-  return go && (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kCancelBit);
+// A pre-armed launch its server cancelled: the server's host-pinned cancel word holds the
+// task's seq (set before the doorbell wait is released, cleared once the stream has
+// drained, so every workgroup of the task reads the same value): return before any work.
+__device__ __forceinline__ bool disarmed(const unsigned long long* go, unsigned long long seq) {
+  return go && __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
 }
 
 }  // namespace dev

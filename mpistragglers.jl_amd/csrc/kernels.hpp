@@ -51,9 +51,9 @@ struct LsqTask {
   unsigned long long seq;
   int64_t rows, lda;
   int cols, grid;
-  // pre-armed launch of a worker process: device copy of the doorbell the
-  // launch waited on; a value with kCancelBit set means "disarmed", and the task returns
-  // without computing or publishing (NULL: not armed)
+  // pre-armed launch of a worker process: the server's cancel word; equal
+  // to seq means "disarmed", and the task returns without computing or publishing (NULL:
+  // not armed)
   const unsigned long long* go;
 };
 constexpr unsigned long long kCancelBit = 1ull << 62;

@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   while (ti + 1 < batch.ntasks && int(blockIdx.x) >= batch.block0[ti + 1]) ++ti;
   const LsqTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block0[ti];
-  if (disarmed(a.go)) return;  // every workgroup of the task alike
+  if (disarmed(a.go, a.seq)) return;  // every workgroup of the task alike
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;

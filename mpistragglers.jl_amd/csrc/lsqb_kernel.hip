@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_chunked_kernel(LsqbBatc
   const int ti = task_of(batch.block1, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block1[ti];
-  if (disarmed(a.go)) return;
+  if (disarmed(a.go, a.seq)) return;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t rows = a.rows;
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   const int ti = task_of(batch.block1, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block1[ti];
-  if (disarmed(a.go)) return;
+  if (disarmed(a.go, a.seq)) return;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t rows = a.rows;
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
   const int ti = task_of(batch.block2, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block2[ti];
-  if (disarmed(a.go)) return;
+  if (disarmed(a.go, a.seq)) return;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nrange = a.nrange, nslice = a.nslice;

@@ -15,7 +15,7 @@ namespace mpa {
 
 namespace {
 constexpr uint64_t kMagic = 0x4D50415348424F58ull;  // "MPASHBOX"
-constexpr uint64_t kVersion = 1;
+constexpr uint64_t kVersion = 2;
 
 size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 }  // namespace

@@ -21,14 +21,35 @@
 
 namespace mpa {
 
+// Message / reply payload path of a worker (BoxHeader::mode), decided by the coordinator
+// at its first post to the worker once both processes have reported their side:
+//   kPathHost    payloads in this segment (host memory; the worker stages the message)
+//   kPathDevice  payloads in device memory over xGMI: the coordinator's kernels store the
+//                message straight into the worker's device message slot, the worker's
+//                task stores its reply into the coordinator's device reply inbox (both
+//                fine-grained allocations shared by HIP IPC handles); doorbell and done
+//                stay here
+enum : uint32_t { kPathPending = 0, kPathHost = 1, kPathDevice = 2 };
+enum : uint32_t { kIpcPending = 0, kIpcOk = 1, kIpcFailed = 2 };
+
 struct alignas(256) BoxHeader {
   unsigned long long doorbell;
   unsigned long long done;
   unsigned long long msg_bytes;    // sizeof(sendbuf) of the posted message (:80)
   unsigned long long reply_bytes;  // bytes of the recv chunk (:81)
   unsigned long long pad[28];
+  // device-memory path set-up
+  int32_t server_dev, coord_dev;  // HIP device of the serving process / of rank 0
+  volatile uint32_t msg_ipc;      // server: kIpc* of exporting its device message slot
+  volatile uint32_t reply_ipc;    // rank 0: kIpc* of exporting the device reply inbox
+  volatile uint32_t reply_open;   // server: kIpc* of opening that inbox
+  volatile uint32_t mode;         // rank 0: kPath*
+  uint32_t pad32[2];
+  char msg_handle[64];    // hipIpcMemHandle_t of the server's message slot
+  char reply_handle[64];  // hipIpcMemHandle_t of rank 0's reply inbox for this worker
+  uint8_t pad2[96];
 };
-static_assert(sizeof(BoxHeader) == 256, "box header is one 256-byte line group");
+static_assert(sizeof(BoxHeader) == 512, "box header is two 256-byte line groups");
 
 struct alignas(256) ShmHeader {
   uint64_t magic;

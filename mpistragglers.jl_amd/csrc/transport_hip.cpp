@@ -66,6 +66,11 @@ constexpr int kLsqbGrid1 = 256;
 constexpr int kLsqbGrid2 = 512;
 constexpr int kLsqbRangeCap = 128;
 
+bool env_off(const char* name) {
+  const char* e = std::getenv(name);
+  return e && *e == '0';
+}
+
 // Process-wide pool of CU-masked streams: communicators come and go (tests create many),
 // but the HSA queues behind their streams are a bounded hardware resource, so a destroyed
 // comm returns its streams here and the next comm reuses them instead of growing the
@@ -138,11 +143,19 @@ struct HipWorker {
   uint8_t* box_msg_dev = nullptr;
   uint8_t* box_reply_dev = nullptr;
   unsigned long long* box_door_dev = nullptr;
-  uint8_t* xslot = nullptr;  // server: device copy of the staged message
+  uint8_t* xslot = nullptr;  // server: the worker's device message slot
+  // device-memory (xGMI) payload path (shm.hpp kPathDevice): coordinator: the server's
+  // message slot opened by IPC, and its own reply inbox; server: rank 0's inbox opened
+  bool path_known = false, path_dev = false;
+  uint8_t* peer_msg = nullptr;
+  uint8_t* reply_inbox = nullptr;
+  uint8_t* peer_reply = nullptr;
   // server, pre-armed task (serve()): armed = task `seq` is queued behind its doorbell;
-  // go_dev = device copy of the doorbell it ran on; counter bases to restore if cancelled
+  // cancel word (host-pinned, device view) of the armed task; counter bases to restore
+  // if cancelled
   bool armed = false;
-  unsigned long long* go_dev = nullptr;
+  unsigned long long* cancel_host = nullptr;
+  unsigned long long* cancel_dev = nullptr;
   // coordinator, launch-ahead: the next post / harvest of this worker is already enqueued
   bool preposted = false, preharvest = false;
   uint32_t arm_sbase = 0, arm_tbase = 0;
@@ -226,6 +239,10 @@ class HipComm final : public Comm {
     std::memset(flags_, 0, sizeof(unsigned long long) * size_t(n + 1));
     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&err_), 64, hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(err_, 0, 64);
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&cancel_), sizeof(unsigned long long) * size_t(n + 1),
+                           hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(cancel_, 0, sizeof(unsigned long long) * size_t(n + 1));
+    xgmi_ = !env_off("MPA_XGMI");
     HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 1)));
     HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 1)));
     err_dev_ = err_;
@@ -245,9 +262,14 @@ class HipComm final : public Comm {
       if (role_ == SERVER && w.here) {
         w.flag_host = &w.box->done;
         w.flag_dev = region_->dev(&w.box->done);
-        HIPCHECK(hipMalloc(&w.xslot, region_->max_msg()));
+        w.box->server_dev = dev_;
+        w.xslot = static_cast<uint8_t*>(ipc_alloc(region_->max_msg(), w.box->msg_handle, &w.box->msg_ipc));
+        w.cancel_host = &cancel_[r - 1];
+        w.cancel_dev = &cancel_[r - 1];
       } else if (w.remote) {
         w.flag_host = &w.box->done;
+        w.box->coord_dev = dev_;
+        w.reply_inbox = static_cast<uint8_t*>(ipc_alloc(region_->max_msg(), w.box->reply_handle, &w.box->reply_ipc));
       } else {
         w.flag_host = &flags_[r - 1];
         w.flag_dev = &flags_[r - 1];
@@ -285,8 +307,10 @@ class HipComm final : public Comm {
       if (w.lsqb_R) (void)hipFree(w.lsqb_R);
       if (w.lsqb_slab) (void)hipFree(w.lsqb_slab);
       if (w.lsqb_ctr) (void)hipFree(w.lsqb_ctr);
+      if (w.peer_msg) (void)hipIpcCloseMemHandle(w.peer_msg);
+      if (w.peer_reply) (void)hipIpcCloseMemHandle(w.peer_reply);
       if (w.xslot) (void)hipFree(w.xslot);
-      if (w.go_dev) (void)hipFree(w.go_dev);
+      if (w.reply_inbox) (void)hipFree(w.reply_inbox);
       if (w.stream) release_queue_stream(dev_, w.stream);
     }
     for (auto& s : launch_streams_) release_queue_stream(dev_, s);
@@ -298,6 +322,7 @@ class HipComm final : public Comm {
     if (ctr_) (void)hipFree(ctr_);
     if (flags_) (void)hipHostFree(flags_);
     if (err_) (void)hipHostFree(err_);
+    if (cancel_) (void)hipHostFree(cancel_);
     if (xfer_ev_) (void)hipEventDestroy(xfer_ev_);
     delete region_;
   }
@@ -328,6 +353,7 @@ class HipComm final : public Comm {
       return;
     }
     if (w.remote) {
+      if (!w.path_known) decide_path(rank);
       if (b_.sl > region_->max_msg() || b_.rl > region_->max_msg())
         fail(MPA_DIMENSION_MISMATCH, "messages of %zu / %zu bytes exceed the communicator's mailbox of %zu bytes",
              b_.sl, b_.rl, region_->max_msg());
@@ -406,7 +432,7 @@ class HipComm final : public Comm {
         if (w.remote) {
           xb.reserve(2, 1);
           xb.copy(b_.sendbuf, slot, b_.sl);
-          xb.copy(b_.sendbuf, w.box_msg_dev, b_.sl);
+          xb.copy(b_.sendbuf, msg_dst(w), b_.sl);
           xb.door(w.box_door_dev, w.seq);
         } else {
           xb.copy(b_.sendbuf, slot, b_.sl);
@@ -437,6 +463,11 @@ class HipComm final : public Comm {
     uint16_t* mirror = nullptr;  // bf16 copy of x; the message when msg_bf16
     bool msg_bf16 = false;
   };
+  int payload_path(int64_t rank) const {
+    if (rank < 1 || rank > nworkers_) return 0;
+    const HipWorker& w = w_[size_t(rank - 1)];
+    return w.remote && w.path_known ? (w.path_dev ? int(kPathDevice) : int(kPathHost)) : 0;
+  }
   // end_call() leaves the call's harvests pending (they join the next flush's epoch kernel)
   void set_defer_end_flush(bool on) { defer_end_ = on; }
   void stage_update(const UpdateSpec& u) {
@@ -519,7 +550,7 @@ class HipComm final : public Comm {
     } disarm_guard{this};
     std::vector<int64_t> fresh;
     for (int64_t r = 1; r <= nworkers_; ++r)
-      if (w_[size_t(r - 1)].here && armable(r)) arm(r);
+      if (w_[size_t(r - 1)].here && server_path(r) && armable(r)) arm(r);
     for (uint64_t spins = 0;; ++spins) {
       if (__atomic_load_n(&h->shutdown, __ATOMIC_ACQUIRE) || __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE) != gen0) break;
       fresh.clear();
@@ -527,6 +558,13 @@ class HipComm final : public Comm {
       for (int64_t r = 1; r <= nworkers_; ++r) {
         HipWorker& w = w_[size_t(r - 1)];
         if (!w.here) continue;
+        if (!w.path_known) {
+          if (server_path(r)) {
+            progress = true;
+            if (armable(r)) arm(r);
+          }
+          continue;
+        }
         if (w.armed) {
           if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) continue;
           // the armed task ran: check what rank 0 posted against what it was armed for
@@ -546,7 +584,7 @@ class HipComm final : public Comm {
         w.rl = size_t(w.box->reply_bytes);
         check_task(r, tasks_[size_t(r - 1)], w.sl, w.rl);
         w.x = w.xslot;
-        w.out = w.box_reply_dev;
+        w.out = reply_dst(w);
         fresh.push_back(r);
       }
       if (!fresh.empty()) {
@@ -591,10 +629,6 @@ class HipComm final : public Comm {
   void arm(int64_t rank) {
     HipWorker& w = w_[size_t(rank - 1)];
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
-    if (!w.go_dev) {
-      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.go_dev), 64));
-      HIPCHECK(hipMemset(w.go_dev, 0, 64));
-    }
     const unsigned long long s = w.seq + 1;
     w.arm_sbase = w.lsqb_sbase;
     w.arm_tbase = w.lsqb_tbase;
@@ -603,40 +637,48 @@ class HipComm final : public Comm {
     w.sl = task_msg_bytes(ts);
     w.rl = w.sl * (ts.kind == MPA_TASK_LSQ_BATCH ? 2 : 1);
     w.x = w.xslot;
-    w.out = w.box_reply_dev;
-    ExchangeBuilder xb(ticket_, &ticket_count_, w.stream);
-    xb.copy(w.box_msg_dev, w.xslot, w.sl);
-    xb.copy(reinterpret_cast<const uint8_t*>(w.box_door_dev), reinterpret_cast<uint8_t*>(w.go_dev), 8);
-    xb.launch();
+    w.out = reply_dst(w);
+    if (!w.path_dev) {  // host mailbox: stage the message into the device slot first
+      ExchangeBuilder xb(ticket_, &ticket_count_, w.stream);
+      xb.copy(w.box_msg_dev, w.xslot, w.sl);
+      xb.launch();
+    }
     double bytes = 0;
     if (ts.kind == MPA_TASK_LSQ) {
       LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes, armed_share());
-      b.t[0].go = w.go_dev;
+      b.t[0].go = w.cancel_dev;
       enqueue_lsq(b, ts.dtype, int(ts.cols), w.stream, bytes, rank);
     } else {
       LsqbBatch b = build_lsqb_batch({rank}, &bytes);
-      b.t[0].go = w.go_dev;
+      b.t[0].go = w.cancel_dev;
       enqueue_lsqb(b, w.stream, bytes, rank);
     }
     w.armed = true;
   }
 
   // release every pending armed wait: a task whose doorbell rank 0 has not rung is
-  // cancelled (doorbell := seq | kCancelBit, then restored), one already rung completes
+  // cancelled (cancel word := its seq, then doorbell := seq | kCancelBit to release the
+  // wait; both restored once the stream has drained), one already rung completes.  A task
+  // cancelled in a race with rank 0's ring did not run: its doorbell is served by the next
+  // serve() session (seq rolled back).
   void disarm_all() {
     if (role_ != SERVER) return;
     for (int64_t r = 1; r <= nworkers_; ++r) {
       HipWorker& w = w_[size_t(r - 1)];
       if (!w.here || !w.armed) continue;
       unsigned long long expect = w.seq - 1;
-      const unsigned long long cancel = w.seq | kCancelBit;
-      const bool cancelled = __atomic_compare_exchange_n(&w.box->doorbell, &expect, cancel, false, __ATOMIC_ACQ_REL,
-                                                         __ATOMIC_ACQUIRE);
+      bool cancelled = false;
+      if (__atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE) < w.seq) {
+        __atomic_store_n(w.cancel_host, w.seq, __ATOMIC_SEQ_CST);
+        cancelled = __atomic_compare_exchange_n(&w.box->doorbell, &expect, w.seq | kCancelBit, false, __ATOMIC_SEQ_CST,
+                                                __ATOMIC_SEQ_CST);
+      }
       (void)hipStreamSynchronize(w.stream);
       if (cancelled) {
-        unsigned long long c2 = cancel;  // restore unless rank 0 rang meanwhile
+        unsigned long long c2 = w.seq | kCancelBit;  // restore unless rank 0 rang meanwhile
         __atomic_compare_exchange_n(&w.box->doorbell, &c2, w.seq - 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
       }
+      __atomic_store_n(w.cancel_host, 0ull, __ATOMIC_SEQ_CST);
       if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) {  // it did not run
         w.seq -= 1;
         w.lsqb_sbase = w.arm_sbase;
@@ -659,7 +701,7 @@ class HipComm final : public Comm {
 
   void add_harvest(ExchangeBuilder& xb, const Harvest& h) {
     const HipWorker& w = w_[size_t(h.rank - 1)];
-    const uint8_t* src = w.remote ? w.box_reply_dev : b_.irecvbuf + size_t(h.slot) * b_.rl;
+    const uint8_t* src = w.remote ? reply_src(w) : b_.irecvbuf + size_t(h.slot) * b_.rl;
     xb.copy(src, b_.recvbuf + size_t(h.slot) * b_.rl, b_.rl);
   }
 
@@ -715,7 +757,7 @@ class HipComm final : public Comm {
     a.recv = b_.recvbuf;
     for (size_t k = 0; k < hv.size(); ++k) {
       const HipWorker& w = w_[size_t(hv[k].rank - 1)];
-      const uint8_t* src = w.remote ? w.box_reply_dev : b_.irecvbuf + size_t(hv[k].slot) * b_.rl;
+      const uint8_t* src = w.remote ? reply_src(w) : b_.irecvbuf + size_t(hv[k].slot) * b_.rl;
       (k < before ? a.hsrc : a.hsrc2)[hv[k].slot] = src;
     }
     for (int64_t i = 0; i < b_.n; ++i) a.w[i] = u.w[size_t(i)];
@@ -727,7 +769,7 @@ class HipComm final : public Comm {
       const HipWorker& w = w_[size_t(rank - 1)];
       a.dst[a.ndst++] = b_.isendbuf + size_t(w.slot) * b_.sl;
       if (w.remote) {
-        a.dst[a.ndst++] = w.box_msg_dev;
+        a.dst[a.ndst++] = msg_dst(w);
         a.door[a.ndoor] = w.box_door_dev;
         a.doorval[a.ndoor++] = w.seq;
       }
@@ -781,6 +823,105 @@ class HipComm final : public Comm {
     ahead_upd_ = u;
     ahead_update_ = true;
   }
+
+  // ---- device-memory (xGMI) payload path (shm.hpp kPathDevice) ----
+  // A fine-grained device buffer exported by a HIP IPC handle into `handle`; `state` tells
+  // the other process whether it may open it.  Falls back to a plain allocation (state
+  // kIpcFailed, payloads then go through the host mailbox) if fine-grained memory or IPC is
+  // unavailable, or with MPA_XGMI=0.
+  void* ipc_alloc(size_t bytes, char* handle, volatile uint32_t* state) {
+    void* p = nullptr;
+    if (xgmi_ && hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) == hipSuccess) {
+      hipIpcMemHandle_t h;
+      if (hipIpcGetMemHandle(&h, p) == hipSuccess) {
+        std::memcpy(handle, &h, sizeof(h));
+        __atomic_store_n(state, kIpcOk, __ATOMIC_RELEASE);
+        return p;
+      }
+      (void)hipGetLastError();
+      std::fprintf(stderr, "[mpa] hipIpcGetMemHandle failed: worker payloads use the host mailbox\n");
+      (void)hipFree(p);
+      p = nullptr;
+    }
+    (void)hipGetLastError();
+    HIPCHECK(hipMalloc(&p, bytes));
+    __atomic_store_n(state, kIpcFailed, __ATOMIC_RELEASE);
+    return p;
+  }
+
+  void* ipc_open(const char* handle, int peer_dev) {
+    if (peer_dev != dev_) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, dev_, peer_dev) != hipSuccess || !can) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+      const hipError_t e = hipDeviceEnablePeerAccess(peer_dev, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+      (void)hipGetLastError();
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof(h));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    return p;
+  }
+
+  // coordinator, first post to a remote worker: once the server has exported its message
+  // slot and opened our reply inbox, open its slot and fix the path for good
+  void decide_path(int64_t rank) {
+    HipWorker& w = w_[size_t(rank - 1)];
+    BoxHeader* b = w.box;
+    const auto t0 = Clock::now();
+    for (uint64_t spins = 0; __atomic_load_n(&b->msg_ipc, __ATOMIC_ACQUIRE) == kIpcPending ||
+                             __atomic_load_n(&b->reply_open, __ATOMIC_ACQUIRE) == kIpcPending;
+         ++spins) {
+      if ((spins & 0xFFF) == 0xFFF) watchdog(t0);
+      __builtin_ia32_pause();
+    }
+    uint32_t mode = kPathHost;
+    if (b->msg_ipc == kIpcOk && b->reply_open == kIpcOk && b->reply_ipc == kIpcOk) {
+      w.peer_msg = static_cast<uint8_t*>(ipc_open(b->msg_handle, b->server_dev));
+      if (w.peer_msg) mode = kPathDevice;
+    }
+    if (mode != kPathDevice && xgmi_)
+      std::fprintf(stderr, "[mpa] worker %lld: device payload path unavailable, using the host mailbox\n",
+                   (long long)rank);
+    w.path_dev = mode == kPathDevice;
+    w.path_known = true;
+    __atomic_store_n(&b->mode, mode, __ATOMIC_RELEASE);
+  }
+
+  // server: open rank 0's reply inbox once it is exported; true once rank 0 fixed the path
+  bool server_path(int64_t rank) {
+    HipWorker& w = w_[size_t(rank - 1)];
+    if (w.path_known) return true;
+    BoxHeader* b = w.box;
+    if (__atomic_load_n(&b->reply_open, __ATOMIC_ACQUIRE) == kIpcPending) {
+      const uint32_t ri = __atomic_load_n(&b->reply_ipc, __ATOMIC_ACQUIRE);
+      if (ri == kIpcPending) return false;
+      if (ri == kIpcOk && b->msg_ipc == kIpcOk) w.peer_reply = static_cast<uint8_t*>(ipc_open(b->reply_handle, b->coord_dev));
+      __atomic_store_n(&b->reply_open, w.peer_reply ? kIpcOk : kIpcFailed, __ATOMIC_RELEASE);
+    }
+    const uint32_t mode = __atomic_load_n(&b->mode, __ATOMIC_ACQUIRE);
+    if (mode == kPathPending) return false;
+    if (mode == kPathDevice && !w.peer_reply) fail(MPA_ERROR, "worker %lld: device path chosen without a reply inbox", (long long)rank);
+    w.path_dev = mode == kPathDevice;
+    w.path_known = true;
+    return true;
+  }
+
+  // where rank 0 stores a remote worker's message / reads its reply
+  uint8_t* msg_dst(const HipWorker& w) const { return w.path_dev ? w.peer_msg : w.box_msg_dev; }
+  const uint8_t* reply_src(const HipWorker& w) const { return w.path_dev ? w.reply_inbox : w.box_reply_dev; }
+  // where a served worker's task writes its reply
+  uint8_t* reply_dst(const HipWorker& w) const { return w.path_dev ? w.peer_reply : w.box_reply_dev; }
 
   bool done(int64_t rank) const {
     const HipWorker& w = w_[size_t(rank - 1)];
@@ -1090,6 +1231,7 @@ class HipComm final : public Comm {
     ExchangeBuilder xb(ticket_, &ticket_count_, s);
     for (int64_t rank : ranks) {
       const HipWorker& w = w_[size_t(rank - 1)];
+      if (w.path_dev) continue;  // rank 0 stored the message into the device slot itself
       if (debug_) {
         std::fprintf(stderr, "[mpa role %d] stage-in worker %lld: %zu bytes %p -> %p\n", int(role_), (long long)rank, w.sl,
                      (void*)w.box_msg_dev, (void*)w.xslot);
@@ -1399,6 +1541,8 @@ class HipComm final : public Comm {
   unsigned long long* flags_ = nullptr;
   unsigned* err_ = nullptr;
   unsigned* err_dev_ = nullptr;
+  unsigned long long* cancel_ = nullptr;  // server: cancel words of armed tasks (host-pinned)
+  bool xgmi_ = true;                      // MPA_XGMI=0: payloads always via the host mailbox
   uint32_t* ctr_ = nullptr;
   uint32_t* ticket_ = nullptr;
   uint32_t ticket_count_ = 0;
@@ -1495,6 +1639,7 @@ void hip_set_ahead(Comm* c, int64_t left, int dtype, int64_t elems, const double
   static_cast<HipComm*>(c)->set_ahead(left, update_spec(dtype, elems, w, n, eta, x, mirror, msg_bf16));
 }
 void hip_flush(Comm* c) { static_cast<HipComm*>(c)->flush(); }
+int hip_payload_path(Comm* c, int64_t rank) { return static_cast<HipComm*>(c)->payload_path(rank); }
 void hip_pause_servers(Comm* c) { static_cast<HipComm*>(c)->pause_servers(); }
 
 }  // namespace mpa

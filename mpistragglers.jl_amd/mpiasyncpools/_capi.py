@@ -56,6 +56,7 @@ SIGNATURES = [
     ("mpa_comm_create_dist", C.c_int, [C.c_int, C.c_int64, _vp, C.c_int, C.c_char_p, _sz, C.POINTER(_vp)]),
     ("mpa_comm_serve", C.c_int, [_vp]),
     ("mpa_comm_pause_servers", C.c_int, [_vp]),
+    ("mpa_comm_payload_path", C.c_int, [_vp, C.c_int64]),
     ("mpa_comm_set_timing", C.c_int, [_vp, C.c_int]),
     ("mpa_comm_timing", C.c_int, [_vp, C.POINTER(C.c_double)]),
     ("mpa_comm_sim_set_compute", C.c_int, [_vp, C.c_int64]),

@@ -209,6 +209,11 @@ class DistComm(DeviceComm):
     def pause_servers(self):
         check(lib().mpa_comm_pause_servers(self._h))
 
+    def payload_path(self, rank):
+        """Rank 0: 'device' (xGMI, HIP IPC), 'host' (shared-memory mailbox) or None
+        (undecided / served here) for worker `rank`."""
+        return {1: "host", 2: "device"}.get(int(lib().mpa_comm_payload_path(self._h, int(rank))))
+
 
 class SimComm(_Comm):
     """Virtual-clock host transport (tests of the state machine only); numpy buffers."""

@@ -367,6 +367,10 @@ def lsq_descent_dist(rank, world, port, placement, env, result_q):
         errors = []
         if pool.epoch != epochs or list(pool.repochs) != [epochs] * n or any(pool.active):
             errors.append(("state", pool.epoch, list(pool.repochs), list(pool.active)))
+        want = "host" if env.get("MPA_XGMI") == "0" else "device"
+        paths = [comm.payload_path(w) for w in range(1, n + 1) if placement[w - 1] != 0]
+        if paths != [want] * len(paths):
+            errors.append(("payload path", paths, want))
         # isendbuf holds the message of the last epoch; recvbuf its harvested replies
         got_isend = isend.clone()
         comm.shutdown()

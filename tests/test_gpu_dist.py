@@ -65,6 +65,8 @@ def test_lsqb_two_processes_prearmed(built):
     ([0, 1], {}),                                         # one worker per process: pre-armed
     ([0, 1, 1], {"MPA_AHEAD": "0"}),                      # fused epoch kernel, no launch-ahead
     ([0, 1], {"MPA_FUSE": "0"}),                          # the unfused loop
+    ([0, 1, 1], {"MPA_XGMI": "0"}),                       # payloads through the host mailbox
+    ([0, 1], {"MPA_XGMI": "0"}),                          # ... pre-armed
 ])
 def test_lsq_descent_two_processes(built, placement, env):
     import torch
