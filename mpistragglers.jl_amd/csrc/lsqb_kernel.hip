@@ -229,6 +229,11 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_chunked_kernel(LsqbBatc
 // next block's fragments already in flight, and the 8 partial residuals are summed in LDS
 // in wave order.  The chunked kernel above re-reads X per row block and walks every row in
 // 256-B pieces 4 KiB apart, which left DRAM pages half used (3.3 TB/s, profiles/).
+// pass-1 A loads: each instruction reads 64 B of 16 rows (the fragment layout), so the other
+// half of every 128-B line is read by the wave's next instruction
+#ifndef LSQB_P1_LOAD
+#define LSQB_P1_LOAD ld16
+#endif
 constexpr int Q_ROWS = 16;
 constexpr int Q_KW = 256;                  // columns per wave
 constexpr int Q_XS = K * 2 + 16;           // LDS bytes per staged X row
@@ -263,6 +268,8 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   uint8_t* stage = lds + wave * Q_STAGE;
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) XF[s][t] = bf16x8{};  // k-steps past cols contribute A x 0
     if (s < nks) {
       // 32 X rows (4 KiB) -> the wave's window: lane moves 16-B pieces l, l+64, ..., l+192
 #pragma unroll
@@ -279,14 +286,22 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   }
   __syncthreads();  // staging windows are reused as the partial-residual buffer below
 
+  // Every load below is unconditional (row, k-step and block clamped to valid addresses,
+  // their contributions zeroed by X = 0 / the row test at use): a load under a branch, or a
+  // select between a fresh load and an old value, made the compiler wait for every load in
+  // flight (s_waitcnt vmcnt(0)) before the MFMAs, which serialised the prefetch with the
+  // compute (3.7 TB/s whatever the cache level).
   typedef bf16x8 Frags[8];
+  const int kc_ok = kc0 < cols ? kc0 : 0;
   auto load_a = [&](Frags& F, int64_t rbx) {
     int64_t r = rbx * Q_ROWS + i;
     r = r < rows ? r : rows - 1;
-    const uint16_t* p = A + r * a.lda + kc0 + 8 * g;
+    const uint16_t* p = A + r * a.lda + kc_ok + 8 * g;
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
-      if (s < nks) F[s] = __builtin_bit_cast(bf16x8, ld16_nt(p + 32 * s));
+    for (int s = 0; s < 8; ++s) {
+      const int sc = s < nks ? s : 0;
+      F[s] = __builtin_bit_cast(bf16x8, LSQB_P1_LOAD(p + 32 * sc));
+    }
   };
   float* part = reinterpret_cast<float*>(lds);  // [wave][16 rows][64 iterates (+4 pad)]
 
@@ -296,8 +311,9 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   auto load_b = [&](uint16_t (&bv)[2], int64_t rbx) {
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const int64_t row = rbx * Q_ROWS + 8 * rg + 2 * h + e;
-      bv[e] = row < rows ? Bm[row * K + it] : uint16_t(0);
+      int64_t row = rbx * Q_ROWS + 8 * rg + 2 * h + e;
+      row = row < rows ? row : rows - 1;  // rows past the end are zeroed at use
+      bv[e] = Bm[row * K + it];
     }
   };
 
@@ -309,18 +325,16 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   auto step = [&](Frags& F, Frags& N, uint16_t (&Bc)[2], uint16_t (&Bn)[2]) -> bool {
     const int64_t rbn = rb + grid1;
     const bool more = rbn < nblocks;
-    if (more) {
-      load_a(N, rbn);
-      load_b(Bn, rbn);
-    }
+    const int64_t rbl = more ? rbn : rb;  // past the last block: re-read this one, unused
+    load_a(N, rbl);
+    load_b(Bn, rbl);
     f32x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 8; ++s)
-      if (s < nks)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = mfma(F[s], XF[s][t], acc[t]);
+      for (int t = 0; t < 4; ++t) acc[t] = mfma(F[s], XF[s][t], acc[t]);
     // lane holds rows 4g + r, iterate 16t + i of this wave's partial
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -366,7 +380,7 @@ constexpr int P2_CW = 256;
 constexpr int P2_AS = P2_CW * 2 + 16;
 constexpr int P2_PART = K * P2_CW;  // floats per workgroup partial
 
-__global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
+__global__ void __launch_bounds__(kThreads, 2) lsqb_grad_kernel(LsqbBatch batch) {
   __shared__ __attribute__((aligned(16))) uint8_t as_[2][32 * P2_AS];
   __shared__ unsigned s_last;
   const int ti = task_of(batch.block2, batch.ntasks);
@@ -386,8 +400,9 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
   const uint8_t* __restrict__ R = static_cast<const uint8_t*>(a.R);
 
   // tile loader: thread t moves 16 B (8 columns) = chunk (t&31) of rows (t>>5) + 8q
-  const int lc = c0 + 8 * (tid & 31);
-  const bool lc_ok = lc < cols;
+  // unconditional loads (see pass 1): columns past cols read column 0 and only feed G
+  // columns that are never stored; steps past the range re-read its last step
+  const int lc = c0 + 8 * (tid & 31) < cols ? c0 + 8 * (tid & 31) : 0;
   typedef uint4 Tile[4];
   typedef bf16x8 RFr[2][4];  // [hi, lo][iterate tile]
   auto load_tile = [&](Tile& T, int64_t s) {
@@ -395,7 +410,7 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
     for (int q = 0; q < 4; ++q) {
       int64_t r = 32 * s + (tid >> 5) + 8 * q;
       r = r < rows ? r : rows - 1;  // rows past the end meet R = 0 (pass 1 zero-fills)
-      T[q] = lc_ok ? ld16_nt(A + r * a.lda + lc) : make_uint4(0, 0, 0, 0);
+      T[q] = ld16_nt(A + r * a.lda + lc);
     }
   };
   auto store_tile = [&](const Tile& T, int buf) {
@@ -423,7 +438,7 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
   int64_t s = s_begin;
   if (s < s_end) {
     load_tile(TA, s);
-    if (s + 1 < s_end) load_tile(TB, s + 1);
+    load_tile(TB, s + 1 < s_end ? s + 1 : s_end - 1);
     load_r(RA, s);
     store_tile(TA, 0);
   }
@@ -432,8 +447,8 @@ __global__ void __launch_bounds__(kThreads) lsqb_grad_kernel(LsqbBatch batch) {
   // step s: LDS buf[cur] holds tile s, Tn holds tile s+1 (in flight), Rc the R fragments of s
   auto step = [&](Tile& Tf, Tile& Tn, RFr& Rc, RFr& Rn) -> bool {
     if (s >= s_end) return false;
-    if (s + 2 < s_end) load_tile(Tf, s + 2);
-    if (s + 1 < s_end) load_r(Rn, s + 1);
+    load_tile(Tf, s + 2 < s_end ? s + 2 : s_end - 1);
+    load_r(Rn, s + 1 < s_end ? s + 1 : s_end - 1);
     bf16x8 bf[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) bf[t] = tr_operand(as_[cur], P2_AS, 0, 2 * (64 * wave + 16 * t), lane);
