@@ -34,6 +34,10 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "iterations/sec + shard-kernel HBM GB/s (% peak), nwait=k of 1/2/4/8 GPUs"
 
 CONFIGS = {
+    # the reference's own CPU example restated on the device: coordinator + 3 workers,
+    # nwait = 2 (examples/iterative_example.jl structure; latency-bound)
+    "c1": dict(rows=3 << 12, cols=64, workers=3, nwait=2, dtype="f64",
+               desc="BASELINE configs[0] shape: 3 workers, fp64 least squares A 3*2^12 x 64, nwait=2 (latency-bound)"),
     "c2": dict(rows=1 << 20, cols=1024, workers=8, nwait=8, dtype="f32",
                desc="BASELINE configs[1]: fp32 least squares A 2^20x1024 row-sharded over 8 logical workers, "
                     "nwait=8 (no stragglers); 1 GPU = 8 stream-workers, N GPUs = 8/N workers per GPU"),
