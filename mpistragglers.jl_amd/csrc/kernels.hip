@@ -116,42 +116,77 @@ __global__ void __launch_bounds__(kThreads) aggregate_kernel(AggregateArgs a) {
 // ---------------------------------------------------------------------------------------
 // The fused coordinator epoch step (EpochArgs).  Same arithmetic as aggregate_kernel (fp64
 // sum in chunk order), so the fused and unfused loops produce identical iterates.
-template <typename T>
+template <typename T, int V>
+struct EVec {
+  T v[V];
+};
+template <typename T, int V>
+__device__ __forceinline__ EVec<T, V> eld(const T* p) {
+  if constexpr (V * sizeof(T) == 16) {
+    return __builtin_bit_cast(EVec<T, V>, *reinterpret_cast<const uint4*>(p));
+  } else {
+    EVec<T, V> r;
+#pragma unroll
+    for (int e = 0; e < V; ++e) r.v[e] = p[e];
+    return r;
+  }
+}
+template <typename T, int V>
+__device__ __forceinline__ void est(T* p, const EVec<T, V>& v) {
+  if constexpr (V * sizeof(T) == 16) *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, v);
+  else
+#pragma unroll
+    for (int e = 0; e < V; ++e) p[e] = v.v[e];
+}
+
+// V elements per thread (16-B vectors when every pointer allows it).  Every chunk load is
+// issued unconditionally before any arithmetic (chunks past n read x, a valid address, and
+// are ignored): a load under a branch made the compiler wait for each one in turn.
+template <typename T, int V>
 __global__ void __launch_bounds__(kThreads) epoch_kernel(EpochArgs a) {
   T* recv = reinterpret_cast<T*>(a.recv);
   T* x = static_cast<T*>(a.x);
-  for (int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j < a.elems;
-       j += int64_t(gridDim.x) * blockDim.x) {
-    T v = x[j];
+  const int64_t nv = a.elems / V;
+  for (int64_t jv = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; jv < nv; jv += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t j = jv * V;
+    EVec<T, V> v = eld<T, V>(x + j);
+    EVec<T, V> c[kMaxEpochChunks];
+#pragma unroll
+    for (int i = 0; i < kMaxEpochChunks; ++i) {
+      const T* src = i < a.n ? (a.hsrc[i] ? reinterpret_cast<const T*>(a.hsrc[i]) : recv + int64_t(i) * a.elems) : x;
+      c[i] = eld<T, V>(src + j);
+    }
+#pragma unroll
+    for (int i = 0; i < kMaxEpochChunks; ++i)
+      if (i < a.n && a.hsrc[i]) est<T, V>(recv + int64_t(i) * a.elems + j, c[i]);
     if (a.update) {
-      double s = 0.0;
-      for (int i = 0; i < a.n; ++i) {
-        T c;
-        if (a.hsrc[i]) {
-          c = reinterpret_cast<const T*>(a.hsrc[i])[j];
-          recv[int64_t(i) * a.elems + j] = c;
-        } else if (a.w[i] != 0.0) {
-          c = recv[int64_t(i) * a.elems + j];
-        } else {
-          continue;
-        }
-        if (a.w[i] != 0.0) s += a.w[i] * double(c);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        double s = 0.0;  // the fp64 sum of aggregate_kernel, in chunk order
+#pragma unroll
+        for (int i = 0; i < kMaxEpochChunks; ++i)
+          if (i < a.n && a.w[i] != 0.0) s += a.w[i] * double(c[i].v[e]);
+        v.v[e] = T(double(v.v[e]) - a.eta * s);
       }
-      v = T(double(v) - a.eta * s);
-      x[j] = v;
-    } else {
-      for (int i = 0; i < a.n; ++i)
-        if (a.hsrc[i]) recv[int64_t(i) * a.elems + j] = reinterpret_cast<const T*>(a.hsrc[i])[j];
+      est<T, V>(x + j, v);
     }
     for (int i = 0; i < a.n; ++i)
-      if (a.hsrc2[i]) recv[int64_t(i) * a.elems + j] = reinterpret_cast<const T*>(a.hsrc2[i])[j];
+      if (a.hsrc2[i]) est<T, V>(recv + int64_t(i) * a.elems + j, eld<T, V>(reinterpret_cast<const T*>(a.hsrc2[i]) + j));
     if (a.msg_bf16) {  // the message is the bf16 mirror (batched variant): a.mirror != NULL
-      const uint16_t h = a.update ? f32_to_bf16_rne(float(v)) : a.mirror[j];
-      if (a.update) a.mirror[j] = h;
-      for (int d = 0; d < a.ndst; ++d) reinterpret_cast<uint16_t*>(a.dst[d])[j] = h;
+      uint16_t h[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) h[e] = a.update ? f32_to_bf16_rne(float(v.v[e])) : a.mirror[j + e];
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (a.update) a.mirror[j + e] = h[e];
+      for (int d = 0; d < a.ndst; ++d)
+#pragma unroll
+        for (int e = 0; e < V; ++e) reinterpret_cast<uint16_t*>(a.dst[d])[j + e] = h[e];
     } else {
-      if (a.update && a.mirror) a.mirror[j] = f32_to_bf16_rne(float(v));
-      for (int d = 0; d < a.ndst; ++d) reinterpret_cast<T*>(a.dst[d])[j] = v;
+      if (a.update && a.mirror)
+#pragma unroll
+        for (int e = 0; e < V; ++e) a.mirror[j + e] = f32_to_bf16_rne(float(v.v[e]));
+      for (int d = 0; d < a.ndst; ++d) est<T, V>(reinterpret_cast<T*>(a.dst[d]) + j, v);
     }
   }
   if (a.ndoor == 0) return;
@@ -238,16 +273,39 @@ hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-int epoch_grid(int64_t elems) {
-  const int64_t g = (elems + kThreads - 1) / kThreads;
+// 16-B vectors when the element count and every pointer the kernel touches allow it
+bool epoch_vec(int dtype, const EpochArgs& a) {
+  const int V = dtype == MPA_F64 ? 2 : 4;
+  uintptr_t m = reinterpret_cast<uintptr_t>(a.recv) | reinterpret_cast<uintptr_t>(a.x);
+  for (int i = 0; i < a.n; ++i)
+    m |= reinterpret_cast<uintptr_t>(a.hsrc[i]) | reinterpret_cast<uintptr_t>(a.hsrc2[i]);
+  if (a.msg_bf16 || a.mirror) {
+    m |= reinterpret_cast<uintptr_t>(a.mirror) & 7u;  // 4 bf16 per thread (8 B)
+    for (int d = 0; d < a.ndst; ++d) m |= reinterpret_cast<uintptr_t>(a.dst[d]) & 7u;
+  }
+  if (!a.msg_bf16)
+    for (int d = 0; d < a.ndst; ++d) m |= reinterpret_cast<uintptr_t>(a.dst[d]);
+  return a.elems % V == 0 && (m & 15u) == 0;
+}
+
+int epoch_grid(int dtype, const EpochArgs& a) {
+  const int V = epoch_vec(dtype, a) ? (dtype == MPA_F64 ? 2 : 4) : 1;
+  const int64_t g = (a.elems / V + kThreads - 1) / kThreads;
   return int(g < 1 ? 1 : g > 1024 ? 1024 : g);
 }
 
 hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s) {
-  const int grid = epoch_grid(a.elems);
-  if (dtype == MPA_F32) hipLaunchKernelGGL(epoch_kernel<float>, dim3(grid), dim3(kThreads), 0, s, a);
-  else if (dtype == MPA_F64) hipLaunchKernelGGL(epoch_kernel<double>, dim3(grid), dim3(kThreads), 0, s, a);
-  else return hipErrorInvalidValue;
+  const int grid = epoch_grid(dtype, a);
+  const bool vec = epoch_vec(dtype, a);
+  if (dtype == MPA_F32) {
+    if (vec) hipLaunchKernelGGL((epoch_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((epoch_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+  } else if (dtype == MPA_F64) {
+    if (vec) hipLaunchKernelGGL((epoch_kernel<double, 2>), dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((epoch_kernel<double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -172,7 +172,7 @@ struct EpochArgs {
   uint32_t ticket_base;
 };
 // grid (blocks) the launch uses: the caller advances the doorbell ticket by it
-int epoch_grid(int64_t elems);
+int epoch_grid(int dtype, const EpochArgs& a);
 hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s);
 
 hipError_t launch_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count,

@@ -777,7 +777,7 @@ class HipComm final : public Comm {
     if (a.ndoor > 0) {
       a.ticket = ticket_;
       a.ticket_base = ticket_count_;
-      ticket_count_ += uint32_t(epoch_grid(a.elems));
+      ticket_count_ += uint32_t(epoch_grid(u.dtype, a));
     }
     HIPCHECK(launch_epoch(u.dtype, a, s));
   }
