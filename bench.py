@@ -44,15 +44,15 @@ CONFIGS = {
     # the other BASELINE configs at their full global size, 8 workers on ONE GPU (secondary
     # measurements and parity cases; the default bench line is c2)
     "c3": dict(rows=1 << 23, cols=2048, workers=8, nwait=6, dtype="f32", delay_mean_ms=1.0,
-               desc="BASELINE configs[2] shape on one GPU: fp32 A 2^23x2048 (8 GiB per worker), nwait=6, "
+               desc="BASELINE configs[2] shape: fp32 A 2^23x2048 (8 GiB per worker), nwait=6, "
                     "injected Exp(1 ms) straggler delays per (worker, task)"),
     "c4": dict(rows=1 << 23, cols=2048, workers=8, nwait="worker1+5", dtype="f64", delay_mean_ms=1.0,
                stale_weight=0.5,
-               desc="BASELINE configs[3] shape on one GPU: fp64 A 2^23x2048 (16 GiB per worker), nwait = "
+               desc="BASELINE configs[3] shape: fp64 A 2^23x2048 (16 GiB per worker), nwait = "
                     "worker 1 fresh + 5 others (test/kmap2.jl:65 style predicate), stale results folded in "
                     "at weight 0.5, Exp(1 ms) delays"),
     "c5": dict(rows=1 << 23, cols=2048, workers=8, nwait=7, dtype="bf16", iterates=64,
-               desc="BASELINE configs[4] shape on one GPU: batched 64-iterate variant, bf16 A 2^23x2048 "
+               desc="BASELINE configs[4] shape: batched 64-iterate variant, bf16 A 2^23x2048 "
                     "(4 GiB per worker), X 2048x64, fp32 accumulate (MFMA), nwait=7"),
 }
 
@@ -201,6 +201,51 @@ def _nwait(M, cfg):
     return nw
 
 
+def register(comm, cfg, seed, w, A, b):
+    """Task (and injected delay schedule) of worker w on the process that serves it."""
+    if cfg.get("iterates", 1) > 1:
+        comm.set_task_lsq_batch(w, A, b)
+    else:
+        comm.set_task_lsq(w, A, b)
+    d = delay_schedule(cfg, seed, w)
+    if d is not None:
+        comm.set_delays(w, d)
+
+
+def max_msg_bytes(cfg):
+    es = {"f32": 4, "f64": 8, "bf16": 2}[cfg["dtype"]]
+    k = cfg.get("iterates", 1)
+    return cfg["cols"] * k * (4 if k > 1 else es)  # the reply is the larger payload
+
+
+def make_loop(M, torch, cfg, pool, comm):
+    """(loop(steps), x): the native coordinator loop of this config on rank 0's buffers."""
+    n, cols, k = cfg["workers"], cfg["cols"], cfg.get("iterates", 1)
+    nwait = _nwait(M, cfg)
+    eta = step_size(cfg["rows"], cols)
+    stale = cfg.get("stale_weight", 0.0)
+    if k > 1:
+        x = torch.zeros(cols * k, device="cuda")          # fp32 master iterate X (cols x 64)
+        xb = torch.zeros(cols * k, dtype=torch.bfloat16, device="cuda")  # its bf16 message
+        isend = torch.zeros(n * cols * k, dtype=torch.bfloat16, device="cuda")
+        recv = torch.zeros(n * cols * k, device="cuda")
+        irecv = torch.zeros_like(recv)
+
+        def loop(steps):
+            M.lsqb_descent(pool, comm, x, xb, recv, isend, irecv, nwait, eta, steps, stale_weight=stale)
+    else:
+        dt = getattr(torch, TORCH_DT[cfg["dtype"]])
+        x = torch.zeros(cols, dtype=dt, device="cuda")
+        isend = torch.zeros(n * cols, dtype=dt, device="cuda")
+        recv = torch.zeros(n * cols, dtype=dt, device="cuda")
+        irecv = torch.zeros_like(recv)
+
+        def loop(steps):
+            M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, eta, steps, stale_weight=stale)
+    loop.bufs = (x, recv, isend, irecv)
+    return loop, x
+
+
 def run_single(args, cfg):
     import torch
     import mpiasyncpools as M
@@ -215,33 +260,11 @@ def run_single(args, cfg):
     torch.cuda.synchronize()
     progress("generated %d shards (%s)" % (n, cfg["config"]))
     for w, (A, b) in enumerate(shards, start=1):
-        if batched:
-            comm.set_task_lsq_batch(w, A, b)
-        else:
-            comm.set_task_lsq(w, A, b)
-        d = delay_schedule(cfg, args.seed, w)
-        if d is not None:
-            comm.set_delays(w, d)
+        register(comm, cfg, args.seed, w, A, b)
     pool = M.MPIAsyncPool(n)
     eta = step_size(cfg["rows"], cols)
-    stale = cfg.get("stale_weight", 0.0)
-    if batched:
-        x = torch.zeros(cols * k, device="cuda")          # fp32 master iterate X (cols x 64)
-        xb = torch.zeros(cols * k, dtype=torch.bfloat16, device="cuda")  # its bf16 message
-        isend = torch.zeros(n * cols * k, dtype=torch.bfloat16, device="cuda")
-        recv = torch.zeros(n * cols * k, device="cuda")
-
-        def loop(steps):
-            M.lsqb_descent(pool, comm, x, xb, recv, isend, irecv, nwait, eta, steps, stale_weight=stale)
-    else:
-        dt = getattr(torch, TORCH_DT[cfg["dtype"]])
-        x = torch.zeros(cols, dtype=dt, device="cuda")
-        isend = torch.zeros(n * cols, dtype=dt, device="cuda")
-        recv = torch.zeros(n * cols, dtype=dt, device="cuda")
-
-        def loop(steps):
-            M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, eta, steps, stale_weight=stale)
-    irecv = torch.zeros_like(recv)
+    loop, x = make_loop(M, torch, cfg, pool, comm)
+    _, recv, isend, irecv = loop.bufs
     extra = {}
     if cfg["config"] == "c2":
         # the same loop from Python (asyncmap_ + weights + lsq_update per step), reported beside
@@ -298,42 +321,32 @@ def run_multi(args, cfg, rank, world, local):
     # MPA_BENCH_ONE_GPU=1 rehearses the N-process path with every rank on GPU 0 (1-GPU box)
     torch.cuda.set_device(0 if os.environ.get("MPA_BENCH_ONE_GPU") == "1" else local)
     dist.init_process_group("gloo")
-    n, cols, nwait = cfg["workers"], cfg["cols"], cfg["nwait"]
+    n = cfg["workers"]
     placement = [(w * world) // n for w in range(n)]  # 8/N consecutive workers per rank
     name = [f"/mpa_bench_{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
     if rank == 0:
-        comm = M.DistComm(n, placement, 0, name[0], cols * 4)
+        comm = M.DistComm(n, placement, 0, name[0], max_msg_bytes(cfg))
     dist.broadcast_object_list(name, src=0)
     if rank != 0:
-        comm = M.DistComm(n, placement, rank, name[0], cols * 4)
+        comm = M.DistComm(n, placement, rank, name[0], max_msg_bytes(cfg))
     keep = []
     for w in range(1, n + 1):
         if placement[w - 1] == rank:
             A, b = gen_shard(M, torch, cfg, args.seed, w)
             keep.append((A, b))
-            comm.set_task_lsq(w, A, b)
+            register(comm, cfg, args.seed, w, A, b)
     torch.cuda.synchronize()
+    if rank == 0:
+        progress("generated rank 0's shards (%s, %d ranks)" % (cfg["config"], world))
     dist.barrier()
     if rank == 0:
         pool = M.MPIAsyncPool(n)
-        x = torch.zeros(cols, device="cuda")
-        isend = torch.zeros(n * cols, device="cuda")
-        recv = torch.zeros(n * cols, device="cuda")
-        irecv = torch.zeros_like(recv)
-        eta = step_size(cfg["rows"], cols)
-        wts = np.zeros(n)
-
-        def step():
-            rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=nwait)
-            fresh = rep == pool.epoch
-            nf = int(fresh.sum())
-            wts[:] = fresh * (n / nf if nf else 0.0)
-            comm.lsq_update(x, recv, n, wts, eta)
-
-        for _ in range(args.warmup):
-            step()
+        loop, x = make_loop(M, torch, cfg, pool, comm)
+        _, recv, isend, irecv = loop.bufs
+        loop(args.warmup)
         M.waitall_(pool, recv, irecv)
         torch.cuda.synchronize()
+        progress("warmup done (%d epochs)" % args.warmup)
         comm.pause_servers()
     else:
         comm.serve()  # warmup session, returns at pause_servers
@@ -343,9 +356,10 @@ def run_multi(args, cfg, rank, world, local):
     dist.barrier()
     t0 = time.perf_counter()
     if rank == 0:
-        M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, eta, args.steps)
+        loop(args.steps)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        fresh = int((pool.repochs == pool.epoch).sum())
         M.waitall_(pool, recv, irecv)
         comm.shutdown()
     else:
@@ -360,8 +374,8 @@ def run_multi(args, cfg, rank, world, local):
     if rank == 0:
         el_max = max(s[0] for s in stats)
         paths = sorted({comm.payload_path(w) for w in range(1, n + 1) if placement[w - 1] != 0} - {None})
-        extra = {"x_norm": float(torch.linalg.norm(x).item()), "build": M.lib().mpa_build_info().decode(),
-                 "placement": placement, "payload_path": "/".join(paths) or None, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None}
+        extra = {"x_norm": float(torch.linalg.norm(x.float()).item()), "build": M.lib().mpa_build_info().decode(),
+                 "fresh_at_last_epoch": fresh, "placement": placement, "payload_path": "/".join(paths) or None, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None}
         print(json.dumps(report(args, cfg, world, el_max, [s[1] for s in stats], extra)), flush=True)
     dist.barrier()
     comm.close()
