@@ -1,0 +1,69 @@
+"""The oracle's state machine over a REAL MPI (MPICH) against its own virtual-clock traces.
+
+oracle/mpi_replay.c runs orc_asyncmap / orc_waitall (the restatement of
+src/MPIAsyncPools.jl:35-224) on rank 0 of an MPICH job whose ranks 1..n run test/kmap2.jl's
+worker program, sleeping each task's scheduled duration.  On the golden schedules whose
+completions are >= 4 ms apart (tests/golden/traces.json, `min_gap_ns`) the trace
+(repochs, active, recvbuf after every call) must equal the virtual-clock trace: this pins the
+oracle's transport model (Isend/Irecv!/Test!/Waitany!/Waitall!) against the MPI library
+MPI.jl binds.  MPICH is outside the repository (this image's /opt/conda); the test is
+skipped where it is absent (the GPU box)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE = os.path.join(ROOT, "oracle")
+MPI_DIR = os.environ.get("MPI_DIR", "/opt/conda")
+MPIEXEC = os.path.join(MPI_DIR, "bin", "mpiexec")
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "traces.json")))["scenarios"]
+SEPARATED = [s["name"] for s in GOLD if s.get("min_gap_ns", 0) >= 4_000_000]
+
+pytestmark = pytest.mark.skipif(not (os.path.exists(os.path.join(MPI_DIR, "include", "mpi.h")) and
+                                     os.path.exists(MPIEXEC)), reason="MPICH not present")
+
+
+@pytest.fixture(scope="module")
+def replay_bin():
+    subprocess.check_call(["make", "-s", "-C", ORACLE, "mpi", f"MPI_DIR={MPI_DIR}"])
+    return os.path.join(ORACLE, "_build", "mpi_replay")
+
+
+def scenario_text(sc):
+    n = sc["n"]
+    dur = sc["durations_ns"]
+    nc = len(dur) // n
+    lines = [f"{n} {nc} {len(sc['ops'])}"]
+    lines += [" ".join(str(x) for x in dur[w * nc:(w + 1) * nc]) for w in range(n)]
+    for op in sc["ops"]:
+        if op["op"] == "waitall":
+            lines.append("W")
+            continue
+        assert "epoch" not in op and "advance_ns" not in op
+        nw = op["nwait"]
+        if isinstance(nw, str):
+            k = int(nw.rsplit("_", 1)[1])
+            lines.append(("F" if nw.startswith("first_plus_") else "C") + f" {k} {op['send']}")
+        else:
+            lines.append(f"A {nw} {op['send']}")
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("name", SEPARATED)
+def test_mpi_replay_matches_virtual_clock_trace(replay_bin, tmp_path, name):
+    sc = next(s for s in GOLD if s["name"] == name)
+    f = tmp_path / "scenario.txt"
+    f.write_text(scenario_text(sc))
+    env = dict(os.environ, HYDRA_LAUNCHER="fork")
+    out = subprocess.run([MPIEXEC, "-n", str(sc["n"] + 1), replay_bin, str(f)], capture_output=True, text=True,
+                         timeout=120, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if "|" in ln]
+    assert len(lines) == len(sc["results"])
+    for k, (ln, ref) in enumerate(zip(lines, sc["results"])):
+        rep, act, rec = ln.split("|")
+        assert [int(v) for v in rep.split()] == ref["repochs"], (name, k, ln)
+        assert [int(v) for v in act.split()] == ref["active"], (name, k, ln)
+        assert [float(v) for v in rec.split()] == ref["recv"], (name, k, ln)
