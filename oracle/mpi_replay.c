@@ -17,6 +17,9 @@
  *                        nops lines: "A <nwait> <send>" | "F <k> <send>" (first_plus_k)
  *                                    | "C <k> <send>" (count_k) | "W" (waitall!)
  * Output, one line per op:  repochs... | active... | recv...
+ * argv[2] (optional): a factor every duration is multiplied by.  Completion order on the
+ * virtual clock depends only on sums of durations along causal chains, so a uniform scale
+ * keeps the trace and widens the gaps against timer and scheduling noise.
  */
 #define _GNU_SOURCE
 #include <mpi.h>
@@ -93,11 +96,12 @@ int main(int argc, char** argv) {
     if (rank == 0) fprintf(stderr, "usage: mpiexec -n <n+1> mpi_replay <scenario>\n");
     MPI_Abort(MPI_COMM_WORLD, 2);
   }
+  const long long scale = argc > 2 ? atoll(argv[2]) : 1;
   int64_t* dur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n * ncols));
   for (long long k = 0; k < n * ncols; ++k) {
     long long v = 0;
     if (fscanf(f, "%lld", &v) != 1) MPI_Abort(MPI_COMM_WORLD, 2);
-    dur[k] = v;
+    dur[k] = v * (scale > 0 ? scale : 1);
   }
 
   MPI_Barrier(MPI_COMM_WORLD);  /* every worker is up before the first post */
@@ -107,7 +111,16 @@ int main(int argc, char** argv) {
     for (int64_t t = 1;; ++t) {
       MPI_Status st;
       double epoch = 0;
-      MPI_Recv(&epoch, 1, MPI_DOUBLE, 0, MPI_ANY_TAG, MPI_COMM_WORLD, &st);
+      /* poll with short sleeps instead of MPICH's spinning receive: n + 1 spinning ranks on
+       * fewer cores delayed the sleepers' wake-ups by milliseconds */
+      MPI_Request rq;
+      MPI_Irecv(&epoch, 1, MPI_DOUBLE, 0, MPI_ANY_TAG, MPI_COMM_WORLD, &rq);
+      for (int done = 0;;) {
+        MPI_Test(&rq, &done, &st);
+        if (done) break;
+        const struct timespec nap = {0, 20000};
+        nanosleep(&nap, NULL);
+      }
       if (st.MPI_TAG == CONTROL_TAG) break;
       const int64_t d = dur[(rank - 1) * ncols + (t - 1) % ncols];
       struct timespec ts = {(time_t)(d / 1000000000), (long)(d % 1000000000)};

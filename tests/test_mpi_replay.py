@@ -57,7 +57,8 @@ def test_mpi_replay_matches_virtual_clock_trace(replay_bin, tmp_path, name):
     f = tmp_path / "scenario.txt"
     f.write_text(scenario_text(sc))
     env = dict(os.environ, HYDRA_LAUNCHER="fork")
-    out = subprocess.run([MPIEXEC, "-n", str(sc["n"] + 1), replay_bin, str(f)], capture_output=True, text=True,
+    # durations x4: the same trace (order depends only on sums of durations), gaps >= 16 ms
+    out = subprocess.run([MPIEXEC, "-n", str(sc["n"] + 1), replay_bin, str(f), "4"], capture_output=True, text=True,
                          timeout=120, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if "|" in ln]
