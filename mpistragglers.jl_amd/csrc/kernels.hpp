@@ -118,6 +118,42 @@ struct LsqbBatch {
 // pass 1 + pass 2 of every task of the batch, two launches on `s`
 hipError_t launch_lsqb(const LsqbBatch& a, hipStream_t s);
 
+// Single-pass variant (lsqf_kernel.hip): groups of P = ceil(cols / kLsqfSlice) workgroups,
+// one 512-column slice each, exchanging per-block partial residuals through `xbuf`.
+constexpr int kLsqfSlice = 512;
+constexpr int kLsqfMaxP = 4;         // cols <= 2048
+constexpr int kLsqfXR = 16;          // exchange ring slots per group
+constexpr int kLsqfMaxGroups = 64;   // per task
+struct LsqfTask {
+  const void* A;
+  const void* B;
+  const void* X;
+  void* out;
+  void* xbuf;                  // [groups][kLsqfXR][P][4][64] f32x4 partial tiles
+  unsigned long long* xflag;   // [groups][kLsqfXR][P]: (seq << 32) | (block + 1)
+  void* slab;                  // [groups][P][128 KiB] G partials
+  uint32_t* ctr;               // [kLsqfMaxP] per-slice group arrivals + [1] slice completions
+  unsigned long long* flag;
+  unsigned long long seq;
+  int64_t rows, lda;
+  int cols;
+  uint32_t sbase, tbase;       // ctr values before this launch
+  const unsigned long long* go;
+};
+struct LsqfBatch {
+  int ntasks;
+  int P;                       // members per group (every task of a batch alike)
+  unsigned* err;
+  unsigned long long spin_ticks;
+  uint32_t* ticket;            // group tickets, monotonic; this launch starts at ticket_base
+  uint32_t ticket_base;
+  int dbg;                     // MPA_LSQF_DBG timing probes: 1 no exchange, 2 also no B (wrong G)
+  int grp0[kMaxLsqTasks + 1];  // groups [grp0[t], grp0[t+1]) serve task t
+  LsqfTask t[kMaxLsqTasks];
+};
+hipError_t launch_lsqf(const LsqfBatch& a, hipStream_t s);
+size_t lsqf_lds_bytes();
+
 struct KmapArgs {
   int kind;
   double rank;

@@ -65,6 +65,7 @@ constexpr int kLaunchStreams = 2;
 constexpr int kLsqbGrid1 = 256;
 constexpr int kLsqbGrid2 = 512;
 constexpr int kLsqbRangeCap = 128;
+constexpr int kLsqfGrid = 256;  // single-pass batched launch: one 768-thread workgroup per CU
 
 bool env_off(const char* name) {
   const char* e = std::getenv(name);
@@ -131,6 +132,12 @@ struct HipWorker {
   size_t lsqb_slab_bytes = 0;
   uint32_t* lsqb_ctr = nullptr;
   uint32_t lsqb_sbase = 0, lsqb_tbase = 0;
+  // single-pass variant (lsqf_kernel.hip): exchange ring, its flags, counters
+  // ([kLsqfMaxP] slices, [1] completions, [1] group tickets) and their running totals
+  void* lsqf_x = nullptr;
+  unsigned long long* lsqf_flag = nullptr;
+  uint32_t* lsqf_ctr = nullptr;
+  uint32_t lsqf_sbase = 0, lsqf_tbase = 0, lsqf_tkt = 0;
   // current task
   int64_t slot = -1;
   const uint8_t* x = nullptr;
@@ -158,7 +165,7 @@ struct HipWorker {
   unsigned long long* cancel_dev = nullptr;
   // coordinator, launch-ahead: the next post / harvest of this worker is already enqueued
   bool preposted = false, preharvest = false;
-  uint32_t arm_sbase = 0, arm_tbase = 0;
+  uint32_t arm_sbase = 0, arm_tbase = 0, arm_fsbase = 0, arm_ftbase = 0, arm_ftkt = 0;
 };
 
 // Accumulates copy items and doorbells into as few exchange launches as fit the kernel
@@ -307,6 +314,9 @@ class HipComm final : public Comm {
       if (w.lsqb_R) (void)hipFree(w.lsqb_R);
       if (w.lsqb_slab) (void)hipFree(w.lsqb_slab);
       if (w.lsqb_ctr) (void)hipFree(w.lsqb_ctr);
+      if (w.lsqf_x) (void)hipFree(w.lsqf_x);
+      if (w.lsqf_flag) (void)hipFree(w.lsqf_flag);
+      if (w.lsqf_ctr) (void)hipFree(w.lsqf_ctr);
       if (w.peer_msg) (void)hipIpcCloseMemHandle(w.peer_msg);
       if (w.peer_reply) (void)hipIpcCloseMemHandle(w.peer_reply);
       if (w.xslot) (void)hipFree(w.xslot);
@@ -632,6 +642,9 @@ class HipComm final : public Comm {
     const unsigned long long s = w.seq + 1;
     w.arm_sbase = w.lsqb_sbase;
     w.arm_tbase = w.lsqb_tbase;
+    w.arm_fsbase = w.lsqf_sbase;
+    w.arm_ftbase = w.lsqf_tbase;
+    w.arm_ftkt = w.lsqf_tkt;
     HIPCHECK(hipStreamWaitValue64(w.stream, w.box_door_dev, s, hipStreamWaitValueGte, ~0ull));
     w.seq = s;
     w.sl = task_msg_bytes(ts);
@@ -649,8 +662,8 @@ class HipComm final : public Comm {
       b.t[0].go = w.cancel_dev;
       enqueue_lsq(b, ts.dtype, int(ts.cols), w.stream, bytes, rank);
     } else {
-      LsqbBatch b = build_lsqb_batch({rank}, &bytes);
-      b.t[0].go = w.cancel_dev;
+      LsqbLaunch b = build_lsqb_batch({rank}, &bytes);
+      b.set_go(w.cancel_dev);
       enqueue_lsqb(b, w.stream, bytes, rank);
     }
     w.armed = true;
@@ -683,6 +696,9 @@ class HipComm final : public Comm {
         w.seq -= 1;
         w.lsqb_sbase = w.arm_sbase;
         w.lsqb_tbase = w.arm_tbase;
+        w.lsqf_sbase = w.arm_fsbase;
+        w.lsqf_tbase = w.arm_ftbase;
+        w.lsqf_tkt = w.arm_ftkt;
         void_timing(r);
       }
       w.armed = false;
@@ -1043,6 +1059,15 @@ class HipComm final : public Comm {
       HIPCHECK(hipMemset(w.lsqb_ctr, 0, sizeof(uint32_t) * (kLsqbMaxSlices + 1)));
       HIPCHECK(hipDeviceSynchronize());
     }
+    if (ts.cols <= kLsqfMaxP * kLsqfSlice && !w.lsqf_x) {
+      const size_t slots = size_t(kLsqfMaxGroups) * kLsqfXR * kLsqfMaxP;
+      HIPCHECK(hipMalloc(&w.lsqf_x, slots * 4 * 64 * 16));
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqf_flag), slots * sizeof(unsigned long long)));
+      HIPCHECK(hipMemset(w.lsqf_flag, 0, slots * sizeof(unsigned long long)));
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqf_ctr), sizeof(uint32_t) * 8));
+      HIPCHECK(hipMemset(w.lsqf_ctr, 0, sizeof(uint32_t) * 8));
+      HIPCHECK(hipDeviceSynchronize());
+    }
   }
 
   // workgroups per task in a least-squares launch of `ntasks` tasks
@@ -1114,7 +1139,7 @@ class HipComm final : public Comm {
         go = [this, b, dt, cols, s, bytes]() { enqueue_lsq(b, dt, cols, s, bytes); };
       } else if (ts.kind == MPA_TASK_LSQ_BATCH) {
         double bytes = 0;
-        const LsqbBatch b = build_lsqb_batch({rank}, &bytes);
+        const LsqbLaunch b = build_lsqb_batch({rank}, &bytes);
         hipStream_t s = w.stream;
         go = [this, b, s, bytes]() { enqueue_lsqb(b, s, bytes); };
       } else {
@@ -1325,19 +1350,100 @@ class HipComm final : public Comm {
 
   void launch_lsqb_batch(const std::vector<int64_t>& ranks, hipStream_t s) {
     double bytes = 0;
-    const LsqbBatch b = build_lsqb_batch(ranks, &bytes);
+    const LsqbLaunch b = build_lsqb_batch(ranks, &bytes);
     enqueue_lsqb(b, s, bytes);
   }
 
-  // kernel arguments of the two launches (pass 1, pass 2) over `ranks`; advances the
-  // workers' counter bases.  Algorithmic bytes per task: A + B + X + G.
-  LsqbBatch build_lsqb_batch(const std::vector<int64_t>& ranks, double* bytes_out) {
-    LsqbBatch b{};
+  // A batched multi-iterate launch: the single-pass kernel (lsqf_kernel.hip) where every
+  // task of the batch has the same slice count (cols <= 2048) and MPA_LSQF is not 0, else
+  // the two passes (lsqb_kernel.hip).
+  struct LsqbLaunch {
+    bool fused = false;
+    LsqbBatch two{};
+    LsqfBatch one{};
+    void set_go(const unsigned long long* go) {
+      if (fused) one.t[0].go = go;
+      else two.t[0].go = go;
+    }
+  };
+
+  bool lsqf_enabled(const std::vector<int64_t>& ranks) const {
+    // opt-in: the single-pass kernel is correct but, as measured, slower
+    // than the two passes
+    const char* e = std::getenv("MPA_LSQF");
+    if (!e || *e != '1') return false;
+    int P = 0;
+    for (int64_t rank : ranks) {
+      const TaskSpec& ts = tasks_[size_t(rank - 1)];
+      const HipWorker& w = w_[size_t(rank - 1)];
+      const int p = int((ts.cols + kLsqfSlice - 1) / kLsqfSlice);
+      if (!w.lsqf_x || p > kLsqfMaxP || (P && p != P)) return false;
+      P = p;
+    }
+    return P > 0;
+  }
+
+  // kernel arguments over `ranks`; advances the workers' counter bases.  Algorithmic bytes
+  // per task: A + B + X + G.
+  LsqbLaunch build_lsqb_batch(const std::vector<int64_t>& ranks, double* bytes_out) {
+    LsqbLaunch L;
+    double bytes = 0;
+    for (int64_t rank : ranks) {
+      const TaskSpec& ts = tasks_[size_t(rank - 1)];
+      bytes += 2.0 * double(ts.rows) * double(ts.cols) + 2.0 * double(ts.rows) * double(ts.k) +
+               2.0 * double(ts.cols) * double(ts.k) + 4.0 * double(ts.cols) * double(ts.k);
+    }
+    *bytes_out = bytes;
+    if (lsqf_enabled(ranks)) {
+      L.fused = true;
+      LsqfBatch& b = L.one;
+      b.ntasks = int(ranks.size());
+      b.err = err_dev_;
+      b.spin_ticks = spin_ticks();
+      { const char* d = std::getenv("MPA_LSQF_DBG"); b.dbg = d ? std::atoi(d) : 0; }
+      b.P = int((tasks_[size_t(ranks[0] - 1)].cols + kLsqfSlice - 1) / kLsqfSlice);
+      // one workgroup per CU: groups of P, dealt evenly over the tasks
+      const int per = std::max(1, std::min(kLsqfMaxGroups, kLsqfGrid / (b.P * b.ntasks)));
+      HipWorker& w0 = w_[size_t(ranks[0] - 1)];
+      b.ticket = w0.lsqf_ctr + kLsqfMaxP + 1;
+      b.ticket_base = w0.lsqf_tkt;
+      int groups = 0;
+      for (int k = 0; k < b.ntasks; ++k) {
+        const int64_t rank = ranks[size_t(k)];
+        HipWorker& w = w_[size_t(rank - 1)];
+        const TaskSpec& ts = tasks_[size_t(rank - 1)];
+        LsqfTask& t = b.t[k];
+        t.A = ts.A;
+        t.B = ts.b;
+        t.X = w.x;
+        t.out = w.out;
+        t.xbuf = w.lsqf_x;
+        t.xflag = w.lsqf_flag;
+        t.slab = w.lsqb_slab;
+        t.ctr = w.lsqf_ctr;
+        t.flag = w.flag_dev;
+        t.seq = w.seq;
+        t.rows = ts.rows;
+        t.lda = ts.lda;
+        t.cols = int(ts.cols);
+        const int64_t nblocks = (ts.rows + 15) / 16;
+        const int ng = int(std::max<int64_t>(1, std::min<int64_t>(per, nblocks)));
+        t.sbase = w.lsqf_sbase;
+        t.tbase = w.lsqf_tbase;
+        w.lsqf_sbase += uint32_t(ng);
+        w.lsqf_tbase += uint32_t(b.P);
+        b.grp0[k] = groups;
+        groups += ng;
+      }
+      b.grp0[b.ntasks] = groups;
+      w0.lsqf_tkt += uint32_t(groups * b.P);
+      return L;
+    }
+    LsqbBatch& b = L.two;
     b.ntasks = int(ranks.size());
     b.err = err_dev_;
     b.spin_ticks = spin_ticks();
     int blocks1 = 0, blocks2 = 0;
-    double bytes = 0;
     const int per1 = std::max(1, kLsqbGrid1 / b.ntasks), per2 = std::max(1, kLsqbGrid2 / b.ntasks);
     b.splitk = 1;
     for (int k = 0; k < b.ntasks; ++k)
@@ -1375,16 +1481,13 @@ class HipComm final : public Comm {
       b.block2[k] = blocks2;
       blocks1 += t.grid1;
       blocks2 += t.nrange * t.nslice;
-      bytes += 2.0 * double(ts.rows) * double(ts.cols) + 2.0 * double(ts.rows) * double(ts.k) +
-               2.0 * double(ts.cols) * double(ts.k) + 4.0 * double(ts.cols) * double(ts.k);
     }
     b.block1[b.ntasks] = blocks1;
     b.block2[b.ntasks] = blocks2;
-    *bytes_out = bytes;
-    return b;
+    return L;
   }
 
-  void enqueue_lsqb(const LsqbBatch& b, hipStream_t s, double bytes, int64_t armed_rank = 0) {
+  void enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int64_t armed_rank = 0) {
     TimedLaunch tl{};
     const bool timed = timing_;
     if (timed) {
@@ -1395,7 +1498,7 @@ class HipComm final : public Comm {
       tl.rank = armed_rank;
       HIPCHECK(hipEventRecord(tl.start, s));
     }
-    HIPCHECK(launch_lsqb(b, s));
+    HIPCHECK(b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
     if (timed) {
       HIPCHECK(hipEventRecord(tl.stop, s));
       std::lock_guard<std::mutex> lk(tm_mu_);
