@@ -145,14 +145,16 @@ struct LsqfBatch {
   int P;                       // members per group (every task of a batch alike)
   unsigned* err;
   unsigned long long spin_ticks;
-  uint32_t* ticket;            // group tickets, monotonic; this launch starts at ticket_base
-  uint32_t ticket_base;
-  int dbg;                     // MPA_LSQF_DBG timing probes: 1 no exchange, 2 also no B (wrong G)
+  unsigned long long* tick;    // [8] per-XCD tickets, [8] arrivals: (tag << 32) | count
+  uint32_t tag;                // this launch's tag (low half of task 0's seq)
+  int lag;                     // phase 1 runs this many blocks ahead (MPA_LSQF_LAG, 1-4)
+  int dbg;                     // MPA_LSQF_DBG: mode 3 loader only, 4 no exchange, 7 all groups cross-XCD; +16 wait profile
   int grp0[kMaxLsqTasks + 1];  // groups [grp0[t], grp0[t+1]) serve task t
   LsqfTask t[kMaxLsqTasks];
 };
 hipError_t launch_lsqf(const LsqfBatch& a, hipStream_t s);
 size_t lsqf_lds_bytes();
+void lsqf_prof_dump();  // MPA_LSQF_DBG & 16: wait-cycle breakdown to stderr
 
 struct KmapArgs {
   int kind;

@@ -66,6 +66,7 @@ constexpr int kLsqbGrid1 = 256;
 constexpr int kLsqbGrid2 = 512;
 constexpr int kLsqbRangeCap = 128;
 constexpr int kLsqfGrid = 256;  // single-pass batched launch: one 768-thread workgroup per CU
+constexpr size_t kLsqfCtrBytes = 64 + 16 * sizeof(unsigned long long);
 
 bool env_off(const char* name) {
   const char* e = std::getenv(name);
@@ -137,7 +138,7 @@ struct HipWorker {
   void* lsqf_x = nullptr;
   unsigned long long* lsqf_flag = nullptr;
   uint32_t* lsqf_ctr = nullptr;
-  uint32_t lsqf_sbase = 0, lsqf_tbase = 0, lsqf_tkt = 0;
+  uint32_t lsqf_sbase = 0, lsqf_tbase = 0;
   // current task
   int64_t slot = -1;
   const uint8_t* x = nullptr;
@@ -165,7 +166,7 @@ struct HipWorker {
   unsigned long long* cancel_dev = nullptr;
   // coordinator, launch-ahead: the next post / harvest of this worker is already enqueued
   bool preposted = false, preharvest = false;
-  uint32_t arm_sbase = 0, arm_tbase = 0, arm_fsbase = 0, arm_ftbase = 0, arm_ftkt = 0;
+  uint32_t arm_sbase = 0, arm_tbase = 0, arm_fsbase = 0, arm_ftbase = 0;
 };
 
 // Accumulates copy items and doorbells into as few exchange launches as fit the kernel
@@ -309,6 +310,7 @@ class HipComm final : public Comm {
     }
     stop_timer();
     (void)hipDeviceSynchronize();
+    if (const char* d = std::getenv("MPA_LSQF_DBG"); d && (std::atoi(d) & 16)) lsqf_prof_dump();
     for (auto& w : w_) {
       if (w.slab) (void)hipFree(w.slab);
       if (w.lsqb_R) (void)hipFree(w.lsqb_R);
@@ -644,7 +646,6 @@ class HipComm final : public Comm {
     w.arm_tbase = w.lsqb_tbase;
     w.arm_fsbase = w.lsqf_sbase;
     w.arm_ftbase = w.lsqf_tbase;
-    w.arm_ftkt = w.lsqf_tkt;
     HIPCHECK(hipStreamWaitValue64(w.stream, w.box_door_dev, s, hipStreamWaitValueGte, ~0ull));
     w.seq = s;
     w.sl = task_msg_bytes(ts);
@@ -698,7 +699,6 @@ class HipComm final : public Comm {
         w.lsqb_tbase = w.arm_tbase;
         w.lsqf_sbase = w.arm_fsbase;
         w.lsqf_tbase = w.arm_ftbase;
-        w.lsqf_tkt = w.arm_ftkt;
         void_timing(r);
       }
       w.armed = false;
@@ -1064,8 +1064,9 @@ class HipComm final : public Comm {
       HIPCHECK(hipMalloc(&w.lsqf_x, slots * 4 * 64 * 16));
       HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqf_flag), slots * sizeof(unsigned long long)));
       HIPCHECK(hipMemset(w.lsqf_flag, 0, slots * sizeof(unsigned long long)));
-      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqf_ctr), sizeof(uint32_t) * 8));
-      HIPCHECK(hipMemset(w.lsqf_ctr, 0, sizeof(uint32_t) * 8));
+      // 8 slice / completion counters, then at byte 64 the per-XCD and arrival ticket words
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqf_ctr), kLsqfCtrBytes));
+      HIPCHECK(hipMemset(w.lsqf_ctr, 0, kLsqfCtrBytes));
       HIPCHECK(hipDeviceSynchronize());
     }
   }
@@ -1401,12 +1402,14 @@ class HipComm final : public Comm {
       b.err = err_dev_;
       b.spin_ticks = spin_ticks();
       { const char* d = std::getenv("MPA_LSQF_DBG"); b.dbg = d ? std::atoi(d) : 0; }
+      { const char* d = std::getenv("MPA_LSQF_LAG"); b.lag = d ? std::atoi(d) : 4; }
       b.P = int((tasks_[size_t(ranks[0] - 1)].cols + kLsqfSlice - 1) / kLsqfSlice);
-      // one workgroup per CU: groups of P, dealt evenly over the tasks
-      const int per = std::max(1, std::min(kLsqfMaxGroups, kLsqfGrid / (b.P * b.ntasks)));
+      // one workgroup per CU: groups of P, as many as keep the grid a multiple of 8 P (the
+      // groups form inside an XCD, 8 XCDs), dealt evenly over the tasks
+      const int target = std::max(1, (kLsqfGrid / b.P) / 8 * 8);
       HipWorker& w0 = w_[size_t(ranks[0] - 1)];
-      b.ticket = w0.lsqf_ctr + kLsqfMaxP + 1;
-      b.ticket_base = w0.lsqf_tkt;
+      b.tick = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(w0.lsqf_ctr) + 64);
+      b.tag = uint32_t(w0.seq);
       int groups = 0;
       for (int k = 0; k < b.ntasks; ++k) {
         const int64_t rank = ranks[size_t(k)];
@@ -1427,7 +1430,8 @@ class HipComm final : public Comm {
         t.lda = ts.lda;
         t.cols = int(ts.cols);
         const int64_t nblocks = (ts.rows + 15) / 16;
-        const int ng = int(std::max<int64_t>(1, std::min<int64_t>(per, nblocks)));
+        const int per = target / b.ntasks + (k < target % b.ntasks ? 1 : 0);
+        const int ng = int(std::max<int64_t>(1, std::min<int64_t>(std::min(per, kLsqfMaxGroups), nblocks)));
         t.sbase = w.lsqf_sbase;
         t.tbase = w.lsqf_tbase;
         w.lsqf_sbase += uint32_t(ng);
@@ -1436,7 +1440,6 @@ class HipComm final : public Comm {
         groups += ng;
       }
       b.grp0[b.ntasks] = groups;
-      w0.lsqf_tkt += uint32_t(groups * b.P);
       return L;
     }
     LsqbBatch& b = L.two;
