@@ -215,6 +215,7 @@ __global__ void __launch_bounds__(F_THREADS) lsqf_kernel(LsqfBatch batch) {
   const unsigned long long ticks = batch.spin_ticks;
   const unsigned long long t0 = rt_now();
   const int mode = batch.dbg & 15;
+  const int skip = mode == 4 ? (batch.dbg >> 8) : 0;  // probe: parts of the no-exchange skeleton left out
   Prof pf{(batch.dbg & 16) != 0, {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
   const unsigned long long c_start = pf.on ? now_cyc() : 0;
   // the group's exchange ring: [XR][P][4 tiles][64 lanes] f32x4 partials, flags [XR][P]
@@ -389,7 +390,7 @@ __global__ void __launch_bounds__(F_THREADS) lsqf_kernel(LsqfBatch batch) {
       const unsigned long long c1 = pf.on ? now_cyc() : 0;
       const uint8_t* base = ring + slot * F_SLOT + i * F_AS + 2 * (256 * kh) + 16 * g;
       f32x4 r1 = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (mode != 8) {
+      if (mode != 8 && !(skip & 1)) {
 #pragma unroll
         for (int s = 0; s < 8; ++s)
           r1 = mfma32(__builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + 64 * s)), XF[s], r1);
@@ -401,13 +402,13 @@ __global__ void __launch_bounds__(F_THREADS) lsqf_kernel(LsqfBatch batch) {
       f32x4* pb = reinterpret_cast<f32x4*>(pairbuf + (t & 1) * F_PAIR) + n * 64 + lane;
       if (kh == 1) {
         // hand the second half to wave n once it has taken block t - 2's out of this buffer
-        if (!lds_wait(&get_cnt[n], unsigned(t > 1 ? t - 1 : 0), t0, ticks, batch.err, pf, 1)) return false;
+        if (!(skip & 8) && !lds_wait(&get_cnt[n], unsigned(t > 1 ? t - 1 : 0), t0, ticks, batch.err, pf, 1)) return false;
         *pb = r1;
         lgkm_drain();
         if (lane == 0) lds_inc(&put_cnt[n]);
         return true;
       }
-      if (!lds_wait(&put_cnt[n], unsigned(t + 1), t0, ticks, batch.err, pf, 2)) return false;
+      if (!(skip & 8) && !lds_wait(&put_cnt[n], unsigned(t + 1), t0, ticks, batch.err, pf, 2)) return false;
       r1 += *pb;  // kh 0 + kh 1, fixed order
       lgkm_drain();
       if (lane == 0) lds_inc(&get_cnt[n]);
@@ -445,14 +446,14 @@ __global__ void __launch_bounds__(F_THREADS) lsqf_kernel(LsqfBatch batch) {
           if (q < P) v += *reinterpret_cast<const f32x4*>(xs + q * 1024 + 16 * lane);
         if (u + 1 < nb) {
           good = load_data(u + 1);
-          if (u + 2 < nb) load_flags(u + 2);
+          if (u + 2 < nb && !(skip & 32)) load_flags(u + 2);
         }
-        good = lds_wait(res_free, unsigned(F_CW) * unsigned(u >= F_NR ? u - F_NR + 1 : 0), t0, ticks, batch.err, pf,
+        good = (skip & 16) || lds_wait(res_free, unsigned(F_CW) * unsigned(u >= F_NR ? u - F_NR + 1 : 0), t0, ticks, batch.err, pf,
                         3) && good;
         const int64_t rb = int64_t(grp) + int64_t(u) * ngroups;
         const int it = 16 * n + i;
         uint16_t hi[4], lo[4];
-        if (mode != 5) {
+        if (mode != 5 && !(skip & 2)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           // B of the block came into the ring slot with A
@@ -470,21 +471,21 @@ __global__ void __launch_bounds__(F_THREADS) lsqf_kernel(LsqfBatch batch) {
         lgkm_drain();
         if (lane == 0) lds_inc(res_cnt);
       }
-      good = lds_wait(res_cnt, 4u * unsigned(u + 1), t0, ticks, batch.err, pf, 3) && good;
+      good = ((skip & 16) || lds_wait(res_cnt, 4u * unsigned(u + 1), t0, ticks, batch.err, pf, 3)) && good;
       const unsigned long long c2 = pf.on ? now_cyc() : 0;
       // phase 2: G^T[it][col] += res^T[it][row] A[row][col], one K = 32 MFMA per tile:
       // k 0-15 the hi residual of rows 0-15, k 16-31 the lo residual of the same rows
       const uint8_t* sb = slot + (8 * (g & 1) + q4) * F_AS + 2 * (64 * cw + 4 * p4);
       bf16x8 bt[4];
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
+      for (int ct = 0; ct < 4 && !(skip & 4); ++ct) {
         // rows 8 (g & 1) + 4 h + q4, columns 64 cw + 16 ct + 4 p4: lane i gets column 16 ct + i
         const s16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sb + 32 * ct));
         const s16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sb + 4 * F_AS + 32 * ct));
         bt[ct] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int uu = 0; uu < 4 && mode != 6; ++uu) {
+      for (int uu = 0; uu < 4 && mode != 6 && !(skip & 4); ++uu) {
         const bf16x8 ra = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(rbuf + (16 * uu + i) * F_RS + 16 * g));
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) acc[uu][ct] = mfma32(ra, bt[ct], acc[uu][ct]);
