@@ -293,6 +293,8 @@ class HipComm final : public Comm {
     timeout_s_ = t ? std::atof(t) : 600.0;
     const char* arm = std::getenv("MPA_ARM");  // unset: auto (armable(); 0 never, 1 always)
     arm_mode_ = arm && *arm == '0' ? 0 : arm && *arm == '1' ? 1 : 2;
+    const char* cb = std::getenv("MPA_COORD_BATCH");
+    coord_batches_ = !(cb && *cb == '0');
     const char* dbg = std::getenv("MPA_DEBUG");
     debug_ = dbg && *dbg == '1';
     if (debug_ && region_) {
@@ -1104,7 +1106,7 @@ class HipComm final : public Comm {
     };
     auto emit = [&]() {
       if (batch.empty()) return;
-      bs = on_coord && !staged ? coord_ : pick_launch_stream();
+      bs = (on_coord || coord_batches_) && !staged ? coord_ : pick_launch_stream();
       if (staged) stage_in(batch, bs);
       else if (bs != coord_) after_exchange(bs);
       if (batch_kind == MPA_TASK_LSQ_BATCH) launch_lsqb_batch(batch, bs);
@@ -1670,6 +1672,10 @@ class HipComm final : public Comm {
   bool timing_ = false;
   bool debug_ = false;
   int arm_mode_ = 2;
+  // undelayed task batches run on the coordinator stream behind the exchange that delivered
+  // their messages (MPA_COORD_BATCH=0: on a launch stream behind a cross-queue event wait,
+  // which measured 75-200 us per hand-off on the k-of-n path, profiles/r01_c1_timeline.txt)
+  bool coord_batches_ = true;
   std::vector<TimedLaunch> timed_;
   std::vector<hipEvent_t> event_pool_;
   int64_t t_launches_ = 0;
