@@ -191,3 +191,30 @@ def test_lsqb_descent_native_loop_matches_python_loop(M, monkeypatch, env):
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a.view(torch.int16) if a.dtype != torch.int16 else a, b.view(torch.int16) if b.dtype != torch.int16 else b)
     assert float(torch.linalg.norm(outs[0][0])) > 0
+
+
+@pytest.mark.parametrize("env", [{"MPA_LSQF": "1"}, {"MPA_LSQF": "1", "MPA_LSQF_DBG": "7"}],
+                         ids=["xcd_local_groups", "cross_xcd_groups"])
+@pytest.mark.parametrize("rows,cols,n", [(1, 32, 1), (4113, 544, 1), (3000, 2048, 3), (20000, 1024, 2)])
+def test_lsqf_single_pass_vs_oracle(M, monkeypatch, env, rows, cols, n):
+    """The opt-in single-pass kernel (lsqf_kernel.hip, MPA_LSQF=1) against the oracle:
+    groups of P = ceil(cols / 512) workgroups exchanging partial residuals, inside an XCD
+    (plain stores through the shared L2) or, with MPA_LSQF_DBG=7, every group treated as
+    spread over XCDs (write-through stores); ragged rows and several tasks per launch.
+    Repeated launches are bitwise identical (fixed member and group summation order)."""
+    import lsq
+    import torch
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    A, B, X = _problem(n * rows, cols, seed=rows + cols + n)
+    shards = [(A[i * rows:(i + 1) * rows - (i * 7 % max(rows, 1) if rows > 7 else 0)],
+               B[i * rows:(i + 1) * rows - (i * 7 % max(rows, 1) if rows > 7 else 0)]) for i in range(n)]
+    out, rep, comm, pool = _run(M, torch, shards, cols, X)
+    assert list(rep) == [1] * n
+    for i, (Ai, Bi) in enumerate(shards):
+        err = lsq.rel_err(out[i], lsq.batched_shard_gradient(Ai, Bi, X, "bf16"))
+        print(f"lsqf rows={Ai.shape[0]} cols={cols} worker {i + 1} rel err {err:.3e}")
+        assert err <= TOL, (i, err)
+    again, _, _, _ = _run(M, torch, shards, cols, X, comm=comm, pool=pool, bufs=comm._bufs)
+    assert np.array_equal(again.view(np.uint32), out.view(np.uint32))
+    comm.close()
