@@ -153,6 +153,28 @@ struct LsqfBatch {
   LsqfTask t[kMaxLsqTasks];
 };
 hipError_t launch_lsqf(const LsqfBatch& a, hipStream_t s);
+
+// Single pass by iterate quarters (lsqq_kernel.hip): quads of workgroups, member q owns
+// iterates 16q..16q+15 of G for all columns (cols <= 2048); no exchange between members.
+struct LsqqTask {
+  const void* A;
+  const void* B;
+  const void* X;
+  void* out;
+  void* slab;                  // [groups][4][ceil(cols/256)][16][64] f32x4 G partials
+  uint32_t* ctr;               // [4] per-member group arrivals, [4] member completions (self-resetting)
+  unsigned long long* flag;
+  unsigned long long seq;
+  int64_t rows, lda;
+  int cols;
+  const unsigned long long* go;
+};
+struct LsqqBatch {
+  int ntasks;
+  int grp0[kMaxLsqTasks + 1];  // quads [grp0[t], grp0[t+1]) serve task t; grid = 4 x quads
+  LsqqTask t[kMaxLsqTasks];
+};
+hipError_t launch_lsqq(const LsqqBatch& a, hipStream_t s);
 size_t lsqf_lds_bytes();
 void lsqf_prof_dump();  // MPA_LSQF_DBG & 16: wait-cycle breakdown to stderr
 

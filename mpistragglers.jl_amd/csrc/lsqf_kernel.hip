@@ -448,8 +448,8 @@ __global__ void __launch_bounds__(F_THREADS) lsqf_kernel(LsqfBatch batch) {
           good = load_data(u + 1);
           if (u + 2 < nb && !(skip & 32)) load_flags(u + 2);
         }
-        good = (skip & 16) || lds_wait(res_free, unsigned(F_CW) * unsigned(u >= F_NR ? u - F_NR + 1 : 0), t0, ticks, batch.err, pf,
-                        3) && good;
+        good = ((skip & 16) || lds_wait(res_free, unsigned(F_CW) * unsigned(u >= F_NR ? u - F_NR + 1 : 0), t0, ticks,
+                                        batch.err, pf, 3)) && good;
         const int64_t rb = int64_t(grp) + int64_t(u) * ngroups;
         const int it = 16 * n + i;
         uint16_t hi[4], lo[4];

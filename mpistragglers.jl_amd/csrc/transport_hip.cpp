@@ -138,6 +138,7 @@ struct HipWorker {
   void* lsqf_x = nullptr;
   unsigned long long* lsqf_flag = nullptr;
   uint32_t* lsqf_ctr = nullptr;
+  uint32_t* lsqq_ctr = nullptr;  // quad kernel: [4] member arrivals, [4] completions (self-resetting)
   uint32_t lsqf_sbase = 0, lsqf_tbase = 0;
   // current task
   int64_t slot = -1;
@@ -321,6 +322,7 @@ class HipComm final : public Comm {
       if (w.lsqf_x) (void)hipFree(w.lsqf_x);
       if (w.lsqf_flag) (void)hipFree(w.lsqf_flag);
       if (w.lsqf_ctr) (void)hipFree(w.lsqf_ctr);
+      if (w.lsqq_ctr) (void)hipFree(w.lsqq_ctr);
       if (w.peer_msg) (void)hipIpcCloseMemHandle(w.peer_msg);
       if (w.peer_reply) (void)hipIpcCloseMemHandle(w.peer_reply);
       if (w.xslot) (void)hipFree(w.xslot);
@@ -1061,6 +1063,10 @@ class HipComm final : public Comm {
       HIPCHECK(hipMemset(w.lsqb_ctr, 0, sizeof(uint32_t) * (kLsqbMaxSlices + 1)));
       HIPCHECK(hipDeviceSynchronize());
     }
+    if (ts.cols <= 2048 && !w.lsqq_ctr) {
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqq_ctr), sizeof(uint32_t) * 8));
+      HIPCHECK(hipMemset(w.lsqq_ctr, 0, sizeof(uint32_t) * 8));
+    }
     if (ts.cols <= kLsqfMaxP * kLsqfSlice && !w.lsqf_x) {
       const size_t slots = size_t(kLsqfMaxGroups) * kLsqfXR * kLsqfMaxP;
       HIPCHECK(hipMalloc(&w.lsqf_x, slots * 4 * 64 * 16));
@@ -1361,14 +1367,28 @@ class HipComm final : public Comm {
   // task of the batch has the same slice count (cols <= 2048) and MPA_LSQF is not 0, else
   // the two passes (lsqb_kernel.hip).
   struct LsqbLaunch {
-    bool fused = false;
+    bool fused = false;  // lsqf (opt-in)
+    bool quad = false;   // lsqq
     LsqbBatch two{};
     LsqfBatch one{};
+    LsqqBatch four{};
     void set_go(const unsigned long long* go) {
-      if (fused) one.t[0].go = go;
+      if (quad) four.t[0].go = go;
+      else if (fused) one.t[0].go = go;
       else two.t[0].go = go;
     }
   };
+
+  // the iterate-quarter single pass (lsqq_kernel.hip): cols <= 2048 on every task
+  bool lsqq_enabled(const std::vector<int64_t>& ranks) const {
+    const char* e = std::getenv("MPA_LSQQ");
+    if (!e || *e != '1') return false;
+    for (int64_t rank : ranks) {
+      const TaskSpec& ts = tasks_[size_t(rank - 1)];
+      if (!w_[size_t(rank - 1)].lsqq_ctr || ts.cols > 2048) return false;
+    }
+    return !ranks.empty();
+  }
 
   bool lsqf_enabled(const std::vector<int64_t>& ranks) const {
     // opt-in: the single-pass kernel is correct but, as measured, slower
@@ -1397,6 +1417,39 @@ class HipComm final : public Comm {
                2.0 * double(ts.cols) * double(ts.k) + 4.0 * double(ts.cols) * double(ts.k);
     }
     *bytes_out = bytes;
+    if (lsqq_enabled(ranks)) {
+      L.quad = true;
+      LsqqBatch& b = L.four;
+      b.ntasks = int(ranks.size());
+      // one 512-thread workgroup per CU: 64 quads (grid 256, a multiple of 32 so that each
+      // quad's members share an XCD), dealt evenly over the tasks
+      constexpr int target = 64;
+      int groups = 0;
+      for (int k = 0; k < b.ntasks; ++k) {
+        const int64_t rank = ranks[size_t(k)];
+        HipWorker& w = w_[size_t(rank - 1)];
+        const TaskSpec& ts = tasks_[size_t(rank - 1)];
+        LsqqTask& t = b.t[k];
+        t.A = ts.A;
+        t.B = ts.b;
+        t.X = w.x;
+        t.out = w.out;
+        t.slab = w.lsqb_slab;
+        t.ctr = w.lsqq_ctr;
+        t.flag = w.flag_dev;
+        t.seq = w.seq;
+        t.rows = ts.rows;
+        t.lda = ts.lda;
+        t.cols = int(ts.cols);
+        const int per = target / b.ntasks + (k < target % b.ntasks ? 1 : 0);
+        const int64_t nblocks = (ts.rows + 15) / 16;
+        const int ng = int(std::max<int64_t>(1, std::min<int64_t>(std::min(per, kLsqfMaxGroups), nblocks)));
+        b.grp0[k] = groups;
+        groups += ng;
+      }
+      b.grp0[b.ntasks] = groups;
+      return L;
+    }
     if (lsqf_enabled(ranks)) {
       L.fused = true;
       LsqfBatch& b = L.one;
@@ -1503,7 +1556,7 @@ class HipComm final : public Comm {
       tl.rank = armed_rank;
       HIPCHECK(hipEventRecord(tl.start, s));
     }
-    HIPCHECK(b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
+    HIPCHECK(b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
     if (timed) {
       HIPCHECK(hipEventRecord(tl.stop, s));
       std::lock_guard<std::mutex> lk(tm_mu_);

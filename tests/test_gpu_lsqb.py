@@ -193,15 +193,16 @@ def test_lsqb_descent_native_loop_matches_python_loop(M, monkeypatch, env):
     assert float(torch.linalg.norm(outs[0][0])) > 0
 
 
-@pytest.mark.parametrize("env", [{"MPA_LSQF": "1"}, {"MPA_LSQF": "1", "MPA_LSQF_DBG": "7"}],
-                         ids=["xcd_local_groups", "cross_xcd_groups"])
+@pytest.mark.parametrize("env", [{"MPA_LSQF": "1"}, {"MPA_LSQF": "1", "MPA_LSQF_DBG": "7"}, {"MPA_LSQQ": "1"}],
+                         ids=["lsqf_xcd_local_groups", "lsqf_cross_xcd_groups", "lsqq_quads"])
 @pytest.mark.parametrize("rows,cols,n", [(1, 32, 1), (4113, 544, 1), (3000, 2048, 3), (20000, 1024, 2)])
-def test_lsqf_single_pass_vs_oracle(M, monkeypatch, env, rows, cols, n):
-    """The opt-in single-pass kernel (lsqf_kernel.hip, MPA_LSQF=1) against the oracle:
-    groups of P = ceil(cols / 512) workgroups exchanging partial residuals, inside an XCD
+def test_single_pass_vs_oracle(M, monkeypatch, env, rows, cols, n):
+    """The opt-in single-pass kernels against the oracle: lsqf_kernel.hip (MPA_LSQF=1),
+    groups of P = ceil(cols / 512) workgroups exchanging partial residuals inside an XCD
     (plain stores through the shared L2) or, with MPA_LSQF_DBG=7, every group treated as
-    spread over XCDs (write-through stores); ragged rows and several tasks per launch.
-    Repeated launches are bitwise identical (fixed member and group summation order)."""
+    spread over XCDs (write-through stores); and lsqq_kernel.hip (MPA_LSQQ=1), quads of
+    workgroups owning 16 iterates each.  Ragged rows and several tasks per launch;
+    repeated launches are bitwise identical (fixed summation orders)."""
     import lsq
     import torch
     for k, v in env.items():
