@@ -171,6 +171,7 @@ struct LsqqTask {
 };
 struct LsqqBatch {
   int ntasks;
+  int dbg;                     // MPA_LSQQ_DBG timing probes (lsqq_kernel.hip)
   int grp0[kMaxLsqTasks + 1];  // quads [grp0[t], grp0[t+1]) serve task t; grid = 4 x quads
   LsqqTask t[kMaxLsqTasks];
 };

@@ -14,16 +14,18 @@
 // Workgroup = 16 waves (4 per SIMD, <= 128 VGPRs each); wave w owns columns
 // [128w, 128w + 128):
 //   phase 1  r_w = A[16 rows][its 128 cols] X[its 128 cols][16 iterates]: 4 MFMAs from A
-//            fragments loaded straight into registers, one block ahead (a second block in
-//            flight spills at 128 VGPRs); the 16 partials are summed in LDS in wave order
-//            and B subtracted: the residual, split bf16 hi + lo;
+//            fragments loaded straight into registers, two blocks ahead; the 16 partials
+//            are summed in LDS in wave order and B subtracted: the residual, split bf16
+//            hi + lo;
 //   phase 2  G^T[16 iterates][its 256 cols] += res^T A: the wave's A fragments are also
 //            written to its own LDS window and read back transposed (ds_read_b64_tr_b16),
 //            one K = 32 MFMA per 16-column tile (k 0-15 hi residual, 16-31 lo residual).
-// Measured (8 workers x 1 GiB, tools/gpu_lsqq.sh): 3.9 ms per batch against 3.3 ms for the
-// two passes, with HBM fetch = 1.04 x the algorithmic bytes (the quad's L2 sharing works):
-// the limit is per-CU latency and the two barriers per block, not HBM.
-// 8 waves (2 per SIMD, 256 VGPRs) ran 4.2 ms, a phase-1 / phase-2 software pipeline 4.5-5.4.
+// Measured (8 workers x 1 GiB, tools/gpu_lsqq.sh, profiles/r01_lsqq.txt): 3.9-4.1 ms per
+// batch against 3.3 ms for the two passes.  HBM fetch is 1.04 x the algorithmic bytes and
+// the L2 hit rate 75 % (the quad's sharing works), but the A loads ALONE (every compute
+// step, barrier and LDS write switched off, MPA_LSQQ_DBG=31) take 4.0 ms: the four-fold
+// L2 -> CU traffic of this layout is delivered at ~8 TB/s chip-wide, so the layout, not
+// the arithmetic or the synchronisation, is the bound.
 //
 // Per-quad-member partial G in a slab, summed over the row groups in group order by the
 // member's last arriver (self-resetting counters), the task's last member publishes.
@@ -75,6 +77,9 @@ __global__ void __launch_bounds__(Q_THREADS) lsqq_kernel(LsqqBatch batch) {
 
   if (batch.ntasks > 0 && disarmed(batch.t[0].go, batch.t[0].seq)) return;
   const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  const int dbg = batch.dbg;  // MPA_LSQQ_DBG timing probes (G wrong): 1 no phase 2, 2 no phase-1
+                              // MFMAs, 4 no residual, 8 no barriers, 16 no
+                              // window writes, 32 no A loads
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // quad member q and global group: same-XCD quads when the grid is a multiple of 32
   const int b = int(blockIdx.x);
@@ -134,6 +139,11 @@ __global__ void __launch_bounds__(Q_THREADS) lsqq_kernel(LsqqBatch batch) {
   };
   const int a_off = int((int64_t(i) * a.lda + c0 + 8 * g) * 2);
   auto load_a = [&](Frags& F, int t) {
+    if (dbg & 32) {  // probe: no A loads
+#pragma unroll
+      for (int s = 0; s < Q_KS; ++s) F[s] = XF[s];
+      return;
+    }
     const auto rs = rsrc(A, blockrow(t), a.lda);
 #pragma unroll
     for (int s = 0; s < Q_KS; ++s)
@@ -149,19 +159,19 @@ __global__ void __launch_bounds__(Q_THREADS) lsqq_kernel(LsqqBatch batch) {
   const int q4 = (lane >> 2) & 3, p4 = lane & 3;
   uint8_t* win = awin[wave];
   auto step = [&](int t, Frags& F, Frags& N, uint16_t& Bc, uint16_t& Bn) {
-    load_a(N, t + 1);
-    Bn = load_b(t + 1);
+    load_a(N, t + 2);
+    Bn = load_b(t + 2);
     // phase 1: this wave's partial residual, and its A fragments into its window
     f32x4 r1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < Q_KS; ++s) r1 = mfma32(F[s], XF[s], r1);
+    for (int s = 0; s < Q_KS && !(dbg & 2); ++s) r1 = mfma32(F[s], XF[s], r1);
 #pragma unroll
-    for (int s = 0; s < Q_KS; ++s) *reinterpret_cast<bf16x8*>(win + i * Q_AS + 64 * s + 16 * g) = F[s];
+    for (int s = 0; s < Q_KS && !(dbg & 16); ++s) *reinterpret_cast<bf16x8*>(win + i * Q_AS + 64 * s + 16 * g) = F[s];
 #pragma unroll
     for (int r = 0; r < 4; ++r) part[wave][(4 * g + r) * Q_PS + i] = r1[r];
-    __syncthreads();
+    if (!(dbg & 8)) __syncthreads();
     // residual = partials in wave order - B, split hi + lo (threads 0-255: row, iterate)
-    if (tid < 256) {
+    if (tid < 256 && !(dbg & 4)) {
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < Q_NW; ++w) v += part[w][rrow * Q_PS + rit];
@@ -171,32 +181,35 @@ __global__ void __launch_bounds__(Q_THREADS) lsqq_kernel(LsqqBatch batch) {
       *reinterpret_cast<uint16_t*>(resimg + rit * Q_RS + 2 * rrow) = hv;
       *reinterpret_cast<uint16_t*>(resimg + rit * Q_RS + 32 + 2 * rrow) = lv;
     }
-    __syncthreads();
+    if (!(dbg & 8)) __syncthreads();
     // phase 2: G^T[16 iterates][c0 + 16 ct + i] += res^T A (K = 16 rows hi + 16 rows lo)
     const bf16x8 ra = *reinterpret_cast<const bf16x8*>(resimg + i * Q_RS + 16 * g);
     const uint8_t* sb = win + (8 * (g & 1) + q4) * Q_AS + 8 * p4;
 #pragma unroll
-    for (int ct = 0; ct < Q_CT; ++ct) {
+    for (int ct = 0; ct < Q_CT && !(dbg & 1); ++ct) {
       const s16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sb + 32 * ct));
       const s16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sb + 4 * Q_AS + 32 * ct));
       const bf16x8 bt = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
       acc[ct] = mfma32(ra, bt, acc[ct]);
       // transposed reads four tiles ahead at most: hoisting all 32 cost 64 VGPRs
-      if ((ct & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      if ((ct & 1) == 1) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
   if (nb > 0) {
-    // two fragment sets in rotation: block t computed while t + 1 is in flight
-    Frags FA, FB;
-    uint16_t BA, BB;
+    Frags FA, FB, FC;
+    uint16_t BA, BB, BC;
     load_a(FA, 0);
     BA = load_b(0);
+    load_a(FB, 1);
+    BB = load_b(1);
     int t = 0;
     for (;;) {
-      step(t, FA, FB, BA, BB);
+      step(t, FA, FC, BA, BC);
       if (++t >= nb) break;
       step(t, FB, FA, BB, BA);
+      if (++t >= nb) break;
+      step(t, FC, FB, BC, BB);
       if (++t >= nb) break;
     }
   }

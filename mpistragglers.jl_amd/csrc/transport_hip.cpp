@@ -1421,6 +1421,7 @@ class HipComm final : public Comm {
       L.quad = true;
       LsqqBatch& b = L.four;
       b.ntasks = int(ranks.size());
+      { const char* d = std::getenv("MPA_LSQQ_DBG"); b.dbg = d ? std::atoi(d) : 0; }
       // one 512-thread workgroup per CU: 64 quads (grid 256, a multiple of 32 so that each
       // quad's members share an XCD), dealt evenly over the tasks
       constexpr int target = 64;
