@@ -317,20 +317,15 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
     }
   };
 
-  // three fragment sets in rotation: the block being computed and the next TWO in flight
-  // (2 x 64 KiB of reads per CU; one block ahead left the CU waiting on HBM latency)
   int64_t rb = blk;
-  Frags FA, FB, FC;
-  uint16_t BA[2], BB[2], BC[2];
-  const int64_t last = blk + (nblocks - 1 - blk) / grid1 * grid1;  // this workgroup's last block
+  Frags FA, FB;
+  uint16_t BA[2], BB[2];
   load_a(FA, rb);
   load_b(BA, rb);
-  load_a(FB, rb + grid1 <= last ? rb + grid1 : last);
-  load_b(BB, rb + grid1 <= last ? rb + grid1 : last);
   auto step = [&](Frags& F, Frags& N, uint16_t (&Bc)[2], uint16_t (&Bn)[2]) -> bool {
     const int64_t rbn = rb + grid1;
     const bool more = rbn < nblocks;
-    const int64_t rbl = rb + 2 * grid1 <= last ? rb + 2 * grid1 : last;  // past the end: re-read, unused
+    const int64_t rbl = more ? rbn : rb;  // past the last block: re-read this one, unused
     load_a(N, rbl);
     load_b(Bn, rbl);
     f32x4 acc[4];
@@ -370,7 +365,7 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
     rb = rbn;
     return more;
   };
-  while (step(FA, FC, BA, BC) && step(FB, FA, BB, BA) && step(FC, FB, BC, BB)) {
+  while (step(FA, FB, BA, BB) && step(FB, FA, BB, BA)) {
   }
 }
 

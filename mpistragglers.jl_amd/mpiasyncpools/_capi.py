@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "_build", "libmpiasyncpools.so")
+# MPA_LIB: another build of the same library (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("MPA_LIB") or os.path.join(PKG_ROOT, "_build", "libmpiasyncpools.so")
 
 MPA_OK, MPA_ARGUMENT_ERROR, MPA_DIMENSION_MISMATCH, MPA_ERROR, MPA_DEVICE_ERROR, MPA_CALLBACK_ERROR = range(6)
 MPA_F32, MPA_F64, MPA_BF16 = 0, 1, 2
