@@ -62,7 +62,7 @@ constexpr int kSlabGridCap = kLsqMaxGrid;  // most workgroups a single task may 
 constexpr int kLaunchStreams = 2;
 // batched multi-iterate task: pass-1 / pass-2 workgroups per launch (= resident: 1 x 512 /
 // 2 x 256 threads per CU by VGPRs), and the most row ranges a pass-2 task is split into
-constexpr int kLsqbGrid1 = 256;
+constexpr int kLsqbGrid1 = 512;  // two 8-wave workgroups per CU: pass 1 4.74-4.88 -> 5.11 TB/s (profiles/r01_lsqb_grid.txt)
 constexpr int kLsqbGrid2 = 512;
 constexpr int kLsqbRangeCap = 128;
 constexpr int kLsqfGrid = 256;  // single-pass batched launch: one 768-thread workgroup per CU
@@ -71,6 +71,13 @@ constexpr size_t kLsqfCtrBytes = 64 + 16 * sizeof(unsigned long long);
 bool env_off(const char* name) {
   const char* e = std::getenv(name);
   return e && *e == '0';
+}
+
+// c5 launch grids (MPA_LSQB_GRID1 / MPA_LSQB_GRID2 override them for measurement)
+int lsqb_grid(int pass) {
+  static const int g1 = [] { const char* e = std::getenv("MPA_LSQB_GRID1"); return e ? std::max(8, std::atoi(e)) : kLsqbGrid1; }();
+  static const int g2 = [] { const char* e = std::getenv("MPA_LSQB_GRID2"); return e ? std::max(8, std::atoi(e)) : kLsqbGrid2; }();
+  return pass == 1 ? g1 : g2;
 }
 
 // Process-wide pool of CU-masked streams: communicators come and go (tests create many),
@@ -1503,7 +1510,7 @@ class HipComm final : public Comm {
     b.err = err_dev_;
     b.spin_ticks = spin_ticks();
     int blocks1 = 0, blocks2 = 0;
-    const int per1 = std::max(1, kLsqbGrid1 / b.ntasks), per2 = std::max(1, kLsqbGrid2 / b.ntasks);
+    const int per1 = std::max(1, lsqb_grid(1) / b.ntasks), per2 = std::max(1, lsqb_grid(2) / b.ntasks);
     b.splitk = 1;
     for (int k = 0; k < b.ntasks; ++k)
       if (tasks_[size_t(ranks[size_t(k)] - 1)].cols > kLsqbSplitKCols) b.splitk = 0;
