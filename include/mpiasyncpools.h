@@ -76,6 +76,8 @@ enum mpa_transport {
   MPA_TRANSPORT_SIM = 1, /* deterministic virtual-clock host transport, for host-logic tests */
   MPA_TRANSPORT_HOST = 2, /* multi-process mailbox protocol with host-executed test workers,
                              for tests of the N > 1 control plane without a GPU */
+  MPA_TRANSPORT_MPI = 3,  /* a real MPI communicator whose ranks run arbitrary worker
+                             programs (libmpiasyncpools_mpi.so, mpiasyncpools_mpi.h) */
 };
 
 enum mpa_nwait_kind { MPA_NWAIT_INT = 0, MPA_NWAIT_FN = 1, MPA_NWAIT_OTHER = 2 };

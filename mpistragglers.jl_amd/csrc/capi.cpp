@@ -41,6 +41,8 @@ struct mpa_comm {
   mpa::Comm* c;
 };
 
+mpa_comm* mpa::adopt_comm(mpa::Comm* c) { return new mpa_comm{c}; }
+
 namespace {
 
 template <typename F>

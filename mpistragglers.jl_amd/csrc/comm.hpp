@@ -76,6 +76,8 @@ class Comm {
 };
 
 Comm* make_sim_comm(int64_t nworkers);
+// wraps a transport built outside this library (libmpiasyncpools_mpi.so) in a C-ABI handle
+::mpa_comm* adopt_comm(Comm* c);
 Comm* make_hip_comm(int64_t nworkers, const int* devices);
 
 }  // namespace mpa

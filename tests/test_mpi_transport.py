@@ -1,0 +1,55 @@
+"""The PRODUCT pool over a real MPI communicator (MPA_TRANSPORT_MPI,
+libmpiasyncpools_mpi.so; SURVEY.md §8f row 3: the reference's workers as arbitrary MPI
+programs).  tests/mpi/pool_mpi_kmap.c runs mpa_asyncmap / mpa_waitall on rank 0 of an
+MPICH job whose ranks 1..n run test/kmap2.jl's worker program, sleeping each task's
+scheduled duration.  On the golden schedules whose completions are >= 4 ms apart
+(tests/golden/traces.json, `min_gap_ns`) the trace (repochs, active, recvbuf after every
+call) must equal the virtual-clock golden trace bit for bit, as the oracle's own replay
+does (tests/test_mpi_replay.py).  MPICH lives outside the repository (this image's
+/opt/conda); the test is skipped where it is absent."""
+import os
+import subprocess
+
+import pytest
+
+from test_mpi_replay import GOLD, MPI_DIR, MPIEXEC, SEPARATED, scenario_text
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "mpistragglers.jl_amd")
+
+pytestmark = pytest.mark.skipif(not (os.path.exists(os.path.join(MPI_DIR, "include", "mpi.h")) and
+                                     os.path.exists(MPIEXEC)), reason="MPICH not present")
+
+
+@pytest.fixture(scope="module")
+def driver():
+    subprocess.check_call(["make", "-s", "-C", PKG, "all", "mpi", f"MPI_DIR={MPI_DIR}"])
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "mpi"), f"MPI_DIR={MPI_DIR}"])
+    return os.path.join(PKG, "_build", "pool_mpi_kmap")
+
+
+def test_mpi_library_exports_its_header(driver):
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(PKG, "_build", "libmpiasyncpools_mpi.so"))
+    from test_capi import MPI_HEADER, declared
+    names = declared([os.path.join(ROOT, "include", MPI_HEADER)])
+    assert names == ["mpa_comm_create_mpi"]
+    assert [n for n in names if not hasattr(lib, n)] == []
+
+
+@pytest.mark.parametrize("name", SEPARATED)
+def test_pool_over_mpi_matches_golden_trace(driver, tmp_path, name):
+    sc = next(s for s in GOLD if s["name"] == name)
+    f = tmp_path / "scenario.txt"
+    f.write_text(scenario_text(sc))
+    env = dict(os.environ, HYDRA_LAUNCHER="fork")
+    out = subprocess.run([MPIEXEC, "-n", str(sc["n"] + 1), driver, str(f), "4"], capture_output=True, text=True,
+                         timeout=120, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if "|" in ln]
+    assert len(lines) == len(sc["results"])
+    for k, (ln, ref) in enumerate(zip(lines, sc["results"])):
+        rep, act, rec = ln.split("|")
+        assert [int(v) for v in rep.split()] == ref["repochs"], (name, k, ln)
+        assert [int(v) for v in act.split()] == ref["active"], (name, k, ln)
+        assert [float(v) for v in rec.split()] == ref["recv"], (name, k, ln)
