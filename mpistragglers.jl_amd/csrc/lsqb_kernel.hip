@@ -231,6 +231,9 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_chunked_kernel(LsqbBatc
 // 256-B pieces 4 KiB apart, which left DRAM pages half used (3.3 TB/s, profiles/).
 // pass-1 A loads: each instruction reads 64 B of 16 rows (the fragment layout), so the other
 // half of every 128-B line is read by the wave's next instruction
+#ifndef LSQB_P1_PROBE
+#define LSQB_P1_PROBE 0
+#endif
 #ifndef LSQB_P1_LOAD
 #define LSQB_P1_LOAD ld16
 #endif
@@ -322,12 +325,24 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   uint16_t BA[2], BB[2];
   load_a(FA, rb);
   load_b(BA, rb);
+#if LSQB_P1_PROBE
+  // measurement only (tools/gpu_p1_probe.sh, profiles/r01_lsqb_p1_probe.txt): 1 = the loads
+  // alone, 2 = loads + MFMAs (no LDS reduction, no barriers); results feed a dead store
+  float sink = 0.f;
+#endif
   auto step = [&](Frags& F, Frags& N, uint16_t (&Bc)[2], uint16_t (&Bn)[2]) -> bool {
     const int64_t rbn = rb + grid1;
     const bool more = rbn < nblocks;
     const int64_t rbl = more ? rbn : rb;  // past the last block: re-read this one, unused
     load_a(N, rbl);
     load_b(Bn, rbl);
+#if LSQB_P1_PROBE == 1
+#pragma unroll
+    for (int s = 0; s < 8; ++s) sink += float(F[s][0]) + float(F[s][7]);
+    sink += float(Bc[0] ^ Bc[1]);
+    rb = rbn;
+    return more;
+#endif
     f32x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -335,6 +350,13 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
     for (int s = 0; s < 8; ++s)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = mfma(F[s], XF[s][t], acc[t]);
+#if LSQB_P1_PROBE == 2
+#pragma unroll
+    for (int t = 0; t < 4; ++t) sink += acc[t][0] + acc[t][3];
+    sink += float(Bc[0] ^ Bc[1]);
+    rb = rbn;
+    return more;
+#endif
     // lane holds rows 4g + r, iterate 16t + i of this wave's partial
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -367,6 +389,9 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   };
   while (step(FA, FB, BA, BB) && step(FB, FA, BB, BA)) {
   }
+#if LSQB_P1_PROBE
+  if (sink == 1234.5f && rows < 0) R[tid] = 1;
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
