@@ -137,6 +137,19 @@ def kernel_name(cfg):
     return "lsq_grad_kernel (one batched launch per epoch per GPU)"
 
 
+def read_peak(M, torch):
+    """Measured HBM read ceiling of this GPU (mpa_read_bandwidth): a plain non-temporal
+    streaming read of a 4 GiB buffer at three grid sizes, best of them, outside the timed
+    region.  Reported beside the spec peak so the roofline fraction can be read against
+    what a read-only kernel reaches on the same box."""
+    buf = torch.empty(1 << 30, dtype=torch.float32, device="cuda")
+    buf.fill_(1.0)
+    best = max(M.read_bandwidth(buf, grid=g, reps=10) for g in (512, 1024, 2048, 4096))
+    del buf
+    torch.cuda.empty_cache()
+    return round(best, 1)
+
+
 def report(args, cfg, world, el, per_rank, extra):
     """per_rank: (launches, summed kernel ms, algorithmic bytes, busy ms) of each GPU.
     roofline.achieved = algorithmic bytes / busy time (the union of the launch intervals, so
@@ -190,6 +203,10 @@ def report(args, cfg, world, el, per_rank, extra):
                      "launches": kl, "busy_ms": round(sum(p[3] for p in per_rank), 3)},
         "epoch_alg_GBps": round(epoch_bytes * its / 1e9, 1),
     }
+    rp = extra.pop("measured_read_peak", None)
+    if rp:
+        out["roofline"]["measured_read_peak"] = rp
+        out["roofline"]["frac_of_measured_read_peak"] = round(achieved / rp, 4) if achieved else None
     out.update(extra)
     return out
 
@@ -300,6 +317,8 @@ def run_single(args, cfg):
     comm.set_timing(False)
     fresh = int((pool.repochs == pool.epoch).sum())
     M.waitall_(pool, recv, irecv)
+    torch.cuda.synchronize()
+    extra["measured_read_peak"] = read_peak(M, torch)
     extra.update({"x_norm": float(torch.linalg.norm(x.float()).item()), "build": M.lib().mpa_build_info().decode(),
                   "loop": "native coordinator loop (mpa_lsq%s_descent)" % ("b" if batched else ""),
                   "fresh_at_last_epoch": fresh})

@@ -241,6 +241,13 @@ int mpa_lsqb_descent(mpa_pool* pool, mpa_comm* comm, void* x32, void* xb16, int6
 int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count,
                  double scale, void* hip_stream);
 
+/* ---- measurement: the HBM read ceiling the roofline is read against ---------------- */
+/* Streams `bytes` (multiple of 16, 16-B aligned device buffer) `reps` times with a plain
+ * non-temporal read kernel of `grid` 256-thread workgroups on `hip_stream` (after one
+ * untimed pass) and returns the rate in GB/s (no reference counterpart: bench.py context
+ * for the shard kernels' roofline fraction, SURVEY.md §8d "measured copy-kernel peak"). */
+int mpa_read_bandwidth(const void* buf, size_t bytes, int grid, int reps, void* hip_stream, double* gbps_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -513,4 +513,30 @@ int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t 
   });
 }
 
+int mpa_read_bandwidth(const void* buf, size_t bytes, int grid, int reps, void* hip_stream, double* gbps_out) {
+  return guarded([&] {
+    if (!buf || bytes < 16 || (bytes & 15) || (reinterpret_cast<uintptr_t>(buf) & 15) || grid < 1 || grid > 65536 ||
+        reps < 1 || !gbps_out)
+      mpa::fail(MPA_ARGUMENT_ERROR, "read_bandwidth: bad arguments");
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    uint32_t* sink = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHECK_C(hipMalloc(&sink, sizeof(uint32_t) * size_t(grid)));
+    hipError_t e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = mpa::launch_read_peak(buf, bytes, grid, sink, s);  // warm-up
+    if (e == hipSuccess) e = hipEventRecord(e0, s);
+    for (int r = 0; r < reps && e == hipSuccess; ++r) e = mpa::launch_read_peak(buf, bytes, grid, sink, s);
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(sink);
+    HIPCHECK_C(e);
+    *gbps_out = ms > 0.f ? double(bytes) * reps / (double(ms) * 1e-3) / 1e9 : 0.0;
+  });
+}
+
 }  // extern "C"

@@ -249,6 +249,32 @@ __global__ void __launch_bounds__(kThreads) generate_kernel(void* out, int dtype
   }
 }
 
+// Measured HBM read ceiling for the roofline context (mpa_read_bandwidth): a streaming
+// read of `n16` 16-B vectors.  Workgroup b reads one contiguous 1/grid of the buffer, 16 KiB
+// per step (four non-temporal 16-B loads in flight per thread, each wave-instruction 1 KiB
+// contiguous), folded into one word per workgroup (the store keeps the loads live).
+__global__ void __launch_bounds__(kThreads) read_peak_kernel(const uint4* __restrict__ p, uint64_t n16,
+                                                             uint32_t* __restrict__ sink) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t lo = per * blockIdx.x, hi = lo + per < n16 ? lo + per : n16;
+  uint32_t x = 0;
+  uint64_t j = lo + threadIdx.x;
+  for (; j + 3 * kThreads < hi; j += 4 * kThreads) {
+    const u32x4 a = __builtin_nontemporal_load(q + j), b = __builtin_nontemporal_load(q + j + kThreads);
+    const u32x4 c = __builtin_nontemporal_load(q + j + 2 * kThreads), d = __builtin_nontemporal_load(q + j + 3 * kThreads);
+    const u32x4 v = a ^ b ^ c ^ d;  // every word used: the loads stay 16 B wide
+    x ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+  }
+  for (; j < hi; j += kThreads) {
+    const u32x4 v = __builtin_nontemporal_load(q + j);
+    x ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+  }
+  x = __reduce_or_sync(0xffffffffffffffffull, x);
+  if (threadIdx.x == 0) sink[blockIdx.x] = x;
+}
+
 }  // namespace
 
 hipError_t launch_exchange(const ExchangeArgs& a, hipStream_t s) {
@@ -316,6 +342,11 @@ hipError_t launch_generate(void* out, int dtype, uint64_t seed, uint32_t stream,
   const uint64_t want = (quads + kThreads - 1) / kThreads;
   const int grid = int(want < 8192 ? want : 8192);
   hipLaunchKernelGGL(generate_kernel, dim3(grid), dim3(kThreads), 0, s, out, dtype, seed, stream, e0, count, scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_peak(const void* p, uint64_t bytes, int grid, uint32_t* sink, hipStream_t s) {
+  hipLaunchKernelGGL(read_peak_kernel, dim3(grid), dim3(kThreads), 0, s, static_cast<const uint4*>(p), bytes / 16, sink);
   return hipGetLastError();
 }
 

@@ -236,6 +236,9 @@ struct EpochArgs {
 int epoch_grid(int dtype, const EpochArgs& a);
 hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s);
 
+// streaming read of `bytes` (a multiple of 16) for the measured HBM read ceiling; `sink`
+// holds `grid` words
+hipError_t launch_read_peak(const void* p, uint64_t bytes, int grid, uint32_t* sink, hipStream_t s);
 hipError_t launch_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count,
                            double scale, hipStream_t s);
 

@@ -26,6 +26,9 @@
 //   M_NT        non-temporal loads of A (streamed once)
 //   M_TREE_FENCE  reduction-tree hand-offs by plain stores + agent release / acquire fences
 //               instead of write-through (sc1) stores and loads
+//   M_BLOCKED   each workgroup streams ONE contiguous row range (its 1/grid of the task,
+//               in whole tiles), its waves taking the range's tiles in turn, instead of
+//               the grid sweeping the task's rows together
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -39,7 +42,7 @@ namespace {
 
 using namespace dev;
 
-enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16 };
+enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16, M_BLOCKED = 32 };
 
 template <typename T>
 struct VecOf;
@@ -235,24 +238,35 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   }
 
   const int64_t rows = a.rows;
-  const int64_t step = int64_t(a.grid) * kWaves * RB;
-  int64_t base = (int64_t(blk) * kWaves + wave) * RB;
+  int64_t step, base, hi;  // this wave's tiles: base, base + step, ... < hi
+  if constexpr (MODE & M_BLOCKED) {
+    const int64_t tile = int64_t(kWaves) * RB;
+    const int64_t per = ((rows + a.grid - 1) / a.grid + tile - 1) / tile * tile;
+    const int64_t lo = int64_t(blk) * per;
+    hi = lo + per < rows ? lo + per : rows;
+    step = tile;
+    base = lo + int64_t(wave) * RB;
+  } else {
+    step = int64_t(a.grid) * kWaves * RB;
+    base = (int64_t(blk) * kWaves + wave) * RB;
+    hi = rows;
+  }
   if constexpr (MODE & M_PREFETCH) {
     Tile<T, VPL, RB, MODE> t0, t1;
-    if (base < rows) t0.load(A, base, rows, a.lda, lane, vok);
+    if (base < hi) t0.load(A, base, rows, a.lda, lane, vok);
     for (;;) {
       const int64_t b1 = base + step;
-      if (base >= rows) break;
-      if (b1 < rows) t1.load(A, b1, rows, a.lda, lane, vok);
+      if (base >= hi) break;
+      if (b1 < hi) t1.load(A, b1, rows, a.lda, lane, vok);
       t0.compute(bv, base, rows, xr, g);
       const int64_t b2 = b1 + step;
-      if (b1 >= rows) break;
-      if (b2 < rows) t0.load(A, b2, rows, a.lda, lane, vok);
+      if (b1 >= hi) break;
+      if (b2 < hi) t0.load(A, b2, rows, a.lda, lane, vok);
       t1.compute(bv, b1, rows, xr, g);
       base = b2;
     }
   } else {
-    for (; base < rows; base += step) {
+    for (; base < hi; base += step) {
       Tile<T, VPL, RB, MODE> t;
       t.load(A, base, rows, a.lda, lane, vok);
       t.compute(bv, base, rows, xr, g);
@@ -398,6 +412,10 @@ constexpr Variant kC2Variants[] = {
     {go<float, 4, 8, M_CLAMP | M_DPP>, 8, "rb8+clamp+dpp"},
     {go<float, 4, 2, M_CLAMP | M_DPP>, 2, "rb2+clamp+dpp"},
     {go<float, 4, 4, M_CLAMP | M_DPP | M_NT | M_TREE_FENCE>, 4, "rb4+clamp+dpp+nt+fenced-tree"},
+    {go<float, 4, 4, M_CLAMP | M_DPP | M_NT | M_BLOCKED>, 4, "rb4+clamp+dpp+nt+blocked"},
+    {go<float, 4, 2, M_CLAMP | M_DPP | M_PREFETCH | M_NT | M_BLOCKED>, 2, "rb2+clamp+dpp+prefetch+nt+blocked"},
+    {go<float, 4, 4, M_CLAMP | M_DPP | M_PREFETCH | M_NT | M_BLOCKED>, 4, "rb4+clamp+dpp+prefetch+nt+blocked"},
+    {go<float, 4, 8, M_CLAMP | M_DPP | M_NT | M_BLOCKED>, 8, "rb8+clamp+dpp+nt+blocked"},
 };
 constexpr int kNumC2Variants = int(sizeof(kC2Variants) / sizeof(kC2Variants[0]));
 constexpr int kDefaultC2 = 5;  // rb4+clamp+dpp+nt: 6.5 TB/s on c2 (profiles/r01_tune.txt)

@@ -57,7 +57,11 @@ int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares la
 namespace {
 
 using Clock = std::chrono::steady_clock;
-constexpr int kDefaultLaunchGrid = 512;  // 2 workgroups per CU: profiles/r01_tune_sweep2.jsonl
+// workgroups per least-squares launch: 192 (24 per XCD, 3/4 of the CUs) streams the c2
+// batch at 7.1-7.2 TB/s against 6.7-6.8 at 512 and 7.0 at 256 (profiles/r01_tune_sweep4_grid.jsonl,
+// same-box bench A/B in profiles/r01_lsq_grid_ab.txt: c2 +6-7 %, c3/c4 unchanged); the read
+// probe (mpa_read_bandwidth) shows the same shape: fewer, longer streams read faster
+constexpr int kDefaultLaunchGrid = 192;
 constexpr int kSlabGridCap = kLsqMaxGrid;  // most workgroups a single task may be given
 constexpr int kLaunchStreams = 2;
 // batched multi-iterate task: pass-1 / pass-2 workgroups per launch (= resident: 1 x 512 /
@@ -1088,7 +1092,8 @@ class HipComm final : public Comm {
 
   // workgroups per task in a least-squares launch of `ntasks` tasks
   int lsq_grid(const TaskSpec& ts, const HipWorker& w, int ntasks) const {
-    const int total = g_lsq_grid > 0 ? g_lsq_grid : kDefaultLaunchGrid;
+    static const int env_grid = [] { const char* e = std::getenv("MPA_LSQ_GRID"); return e ? std::atoi(e) : 0; }();
+    const int total = g_lsq_grid > 0 ? g_lsq_grid : env_grid > 0 ? env_grid : kDefaultLaunchGrid;
     const int rpw = lsq_rows_per_wave_iter(ts.dtype, int(ts.cols));
     const int64_t want = (ts.rows + 4 * rpw - 1) / (4 * rpw);
     int g = total / (ntasks > 0 ? ntasks : 1);

@@ -3,11 +3,11 @@
 completion words.  See DESIGN.md at the repository root.
 """
 from ._capi import lib  # noqa: F401  (fails loudly if the HIP library is not built)
-from .comm import DeviceComm, DistComm, SimComm, generate  # noqa: F401
+from .comm import DeviceComm, DistComm, SimComm, generate, read_bandwidth  # noqa: F401
 from .pool import (ArgumentError, DeviceError, DimensionMismatch, ErrorException,  # noqa: F401
                    MPIAsyncPool, asyncmap, asyncmap_, first_plus, lsq_descent, lsqb_descent, waitall, waitall_)
 
 lib()
 
 __all__ = ["MPIAsyncPool", "asyncmap_", "waitall_", "asyncmap", "waitall", "lsq_descent", "lsqb_descent", "first_plus", "DeviceComm", "DistComm",
-           "SimComm", "generate", "ArgumentError", "DimensionMismatch", "ErrorException", "DeviceError"]
+           "SimComm", "generate", "read_bandwidth", "ArgumentError", "DimensionMismatch", "ErrorException", "DeviceError"]

@@ -72,6 +72,7 @@ SIGNATURES = [
     ("mpa_lsqb_descent", C.c_int, [_vp, _vp, _vp, _vp, C.c_int64, _vp, _vp, _vp, C.c_int, C.c_int64, _vp, _vp,
                                    C.c_double, C.c_double, C.c_int64]),
     ("mpa_generate", C.c_int, [_vp, C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_int64, C.c_double, _vp]),
+    ("mpa_read_bandwidth", C.c_int, [_vp, C.c_size_t, C.c_int, C.c_int, _vp, C.POINTER(C.c_double)]),
 ]
 
 _lib = None

@@ -236,3 +236,14 @@ def generate(out, seed, stream, e0, scale=1.0):
     import torch
     check(lib().mpa_generate(C.c_void_p(out.data_ptr()), dtype_code(out), int(seed), int(stream), int(e0),
                              int(out.numel()), float(scale), C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+
+
+def read_bandwidth(buf, grid=2048, reps=10):
+    """Measured HBM read rate (GB/s) of a plain streaming read over a CUDA tensor's bytes
+    (mpa_read_bandwidth): the ceiling bench.py reads the shard kernels' rate against."""
+    import torch
+    out = C.c_double()
+    nbytes = buf.numel() * buf.element_size() // 16 * 16
+    check(lib().mpa_read_bandwidth(C.c_void_p(buf.data_ptr()), nbytes, int(grid), int(reps),
+                                   C.c_void_p(torch.cuda.current_stream().cuda_stream), C.byref(out)))
+    return out.value

@@ -321,7 +321,10 @@ def lsq_descent_dist(rank, world, port, placement, env, result_q):
     """The native descent loop (fused epoch kernel; launch-ahead at nwait = n: the next
     epoch's doorbells queued behind stream waits on the remote completion words) with
     workers on several processes, against the same loop run by Python in one process on
-    the same shards: identical iterates, bitwise."""
+    the same shards: identical iterates, bitwise.  A task's summation grouping follows its
+    launch grid (a share of the launch, capped at rows / 16 workgroups), and the two runs
+    batch the tasks differently, so the shards are small enough (512 rows: 32 workgroups)
+    that every task runs the same grid in both runs."""
     import numpy as np
     try:
         os.environ.update(env)
@@ -329,7 +332,7 @@ def lsq_descent_dist(rank, world, port, placement, env, result_q):
         import torch
         torch.cuda.set_device(0)
         import mpiasyncpools as M
-        n, rows, cols, seed, epochs, eta = len(placement), 2048, 1024, 23, 7, 0.02
+        n, rows, cols, seed, epochs, eta = len(placement), 512, 1024, 23, 7, 0.02
         name = [f"/mpa_d{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
         if rank == 0:
             comm = M.DistComm(n, placement, 0, name[0], cols * 4, transport="hip")

@@ -56,6 +56,9 @@ def test_errors_without_device(built):
     assert b"unknown transport" in lib().mpa_last_error()
     assert lib().mpa_tune(b"nope", 1) == MPA_ARGUMENT_ERROR
     assert b"unknown tuning key" in lib().mpa_last_error()
+    out = ctypes.c_double()
+    assert lib().mpa_read_bandwidth(None, 1 << 20, 1024, 1, None, ctypes.byref(out)) == MPA_ARGUMENT_ERROR
+    assert b"read_bandwidth: bad arguments" in lib().mpa_last_error()
 
 
 def test_kernel_object_is_gfx950_only(built):

@@ -372,3 +372,15 @@ def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod, monkeypatch, 
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     xs = [xs[0][0], xs[1][0]]
     assert float(torch.linalg.norm(xs[0])) > 0
+
+
+def test_read_bandwidth_probe(M, torch_mod):
+    """mpa_read_bandwidth (bench.py's measured read ceiling) reads every byte and reports a
+    rate inside what the part can do (below the 8 TB/s spec peak, above a floor)."""
+    torch = torch_mod
+    buf = torch.ones(1 << 26, dtype=torch.float32, device="cuda")  # 256 MiB
+    for grid in (256, 2048):
+        gbps = M.read_bandwidth(buf, grid=grid, reps=3)
+        assert 500.0 < gbps < 9000.0, (grid, gbps)
+    with pytest.raises(M.ArgumentError):
+        M.read_bandwidth(buf, grid=0)
