@@ -12,8 +12,8 @@ cd /tmp && export TMPDIR=/tmp
 for k in 1 2; do
   for v in ${VARIANTS:-base p1probe1 p1probe2}; do
     P1=
-    if [ $v = base ] || [ $v = async ]; then L=$R/mpistragglers.jl_amd/_build/libmpiasyncpools.so; else L=$R/mpistragglers.jl_amd/_build/ab/$v/libmpiasyncpools.so; fi
-    [ $v = async ] && P1=async
+    if [ $v = base ] || [ $v = async ] || [ $v = pair ]; then L=$R/mpistragglers.jl_amd/_build/libmpiasyncpools.so; else L=$R/mpistragglers.jl_amd/_build/ab/$v/libmpiasyncpools.so; fi
+    { [ $v = async ] || [ $v = pair ]; } && P1=$v
     MPA_LSQB_P1=$P1 MPA_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/$v$k -o m -- python3 $R/tools/lsqb_mall_probe.py 262144 > $O/$v$k.log 2>&1 || exit $?
   done
 done
