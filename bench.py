@@ -150,6 +150,21 @@ def read_peak(M, torch):
     return round(best, 1)
 
 
+def exchange_report(xt):
+    """The coordinator's epoch kernels in the timed region (mpa_comm_exchange_timing): the
+    broadcast of the iterate to the idle workers and the gather of their replies happen
+    inside them; `remote_*` counts the bytes that crossed to other processes' GPUs (over
+    xGMI at N > 1; 0 at N = 1).  Payloads are cols x 4 B per worker, so the rate is
+    latency-bound, not link-bound (xGMI ~153 GB/s per link)."""
+    launches, ms, remote = xt
+    if not launches:
+        return None
+    return {"kernel": "epoch_kernel (harvest + iterate update + dispatch, coordinator GPU)",
+            "launches": launches, "avg_us": round(ms / launches * 1e3, 2),
+            "remote_bytes_per_launch": remote / launches,
+            "remote_GBps": round(remote / (ms / 1e3) / 1e9, 3) if ms > 0 else None}
+
+
 def report(args, cfg, world, el, per_rank, extra):
     """per_rank: (launches, summed kernel ms, algorithmic bytes, busy ms) of each GPU.
     roofline.achieved = algorithmic bytes / busy time (the union of the launch intervals, so
@@ -315,6 +330,7 @@ def run_single(args, cfg):
     el = time.perf_counter() - t0
     timing = comm.timing()
     comm.set_timing(False)
+    extra["exchange"] = exchange_report(comm.exchange_timing())
     fresh = int((pool.repochs == pool.epoch).sum())
     M.waitall_(pool, recv, irecv)
     torch.cuda.synchronize()
@@ -387,6 +403,7 @@ def run_multi(args, cfg, rank, world, local):
         el = time.perf_counter() - t0
     timing = comm.timing()
     comm.set_timing(False)
+    xch = exchange_report(comm.exchange_timing()) if rank == 0 else None
     dist.barrier()
     stats = [None] * world
     dist.all_gather_object(stats, (el, timing))
@@ -394,7 +411,8 @@ def run_multi(args, cfg, rank, world, local):
         el_max = max(s[0] for s in stats)
         paths = sorted({comm.payload_path(w) for w in range(1, n + 1) if placement[w - 1] != 0} - {None})
         extra = {"x_norm": float(torch.linalg.norm(x.float()).item()), "build": M.lib().mpa_build_info().decode(),
-                 "fresh_at_last_epoch": fresh, "placement": placement, "payload_path": "/".join(paths) or None, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None}
+                 "fresh_at_last_epoch": fresh, "placement": placement, "payload_path": "/".join(paths) or None, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None,
+                 "exchange": xch}
         print(json.dumps(report(args, cfg, world, el_max, [s[1] for s in stats], extra)), flush=True)
     dist.barrier()
     comm.close()

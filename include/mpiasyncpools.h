@@ -199,6 +199,12 @@ int mpa_comm_payload_path(mpa_comm* comm, int64_t rank);
  * delayed workers run concurrently). */
 int mpa_comm_set_timing(mpa_comm* comm, int enable);
 int mpa_comm_timing(mpa_comm* comm, double out[4]);
+/* The coordinator's epoch kernels (fused harvest + update + dispatch, the native descent
+ * loop) timed under the same switch: out = {launches, total ms, bytes moved to / from
+ * workers of OTHER processes (messages into their device slots over xGMI, replies from
+ * their inboxes)} since the previous call.  The broadcast of the iterate
+ * (src/MPIAsyncPools.jl:130-138's Isend to every idle worker) is this kernel's remote part. */
+int mpa_comm_exchange_timing(mpa_comm* comm, double out[3]);
 /* SIM transport only: compute time per task and the virtual clock */
 int mpa_comm_sim_set_compute(mpa_comm* comm, int64_t compute_ns);
 int mpa_comm_sim_advance(mpa_comm* comm, int64_t dt_ns);

@@ -18,6 +18,7 @@ void hip_set_stream(Comm* c, void* s);
 void* hip_get_stream(Comm* c);
 void hip_set_timing(Comm* c, bool on);
 void hip_timing(Comm* c, double out[4]);
+void hip_exchange_timing(Comm* c, double out[3]);
 extern int g_lsq_grid;
 Comm* make_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg);
 void hip_serve(Comm* c);
@@ -315,6 +316,15 @@ int mpa_comm_timing(mpa_comm* comm, double out[4]) {
     need_hip(c);
     if (!out) mpa::fail(MPA_ARGUMENT_ERROR, "out is NULL");
     mpa::hip_timing(&c, out);
+  });
+}
+
+int mpa_comm_exchange_timing(mpa_comm* comm, double out[3]) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    if (!out) mpa::fail(MPA_ARGUMENT_ERROR, "out is NULL");
+    mpa::hip_exchange_timing(&c, out);
   });
 }
 

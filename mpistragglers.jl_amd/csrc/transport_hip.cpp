@@ -810,6 +810,24 @@ class HipComm final : public Comm {
       a.ticket_base = ticket_count_;
       ticket_count_ += uint32_t(epoch_grid(u.dtype, a));
     }
+    if (timing_) {
+      // the exchange this kernel performs over xGMI: messages into remote workers' slots
+      // and replies read from their inboxes (mpa_comm_exchange_timing)
+      double remote = 0;
+      for (int64_t rank : posted)
+        if (w_[size_t(rank - 1)].remote) remote += double(b_.sl);
+      for (const Harvest& h : hv)
+        if (w_[size_t(h.rank - 1)].remote) remote += double(b_.rl);
+      XTimed xt{};
+      xt.start = take_event();
+      xt.stop = take_event();
+      xt.remote_bytes = remote;
+      HIPCHECK(hipEventRecord(xt.start, s));
+      HIPCHECK(launch_epoch(u.dtype, a, s));
+      HIPCHECK(hipEventRecord(xt.stop, s));
+      xtimed_.push_back(xt);
+      return;
+    }
     HIPCHECK(launch_epoch(u.dtype, a, s));
   }
 
@@ -1636,6 +1654,7 @@ class HipComm final : public Comm {
     out[1] = t_ms_;
     out[2] = t_bytes_;
     out[3] = busy;
+    reap_xtiming();
     t_launches_ = 0;
     t_ms_ = 0;
     t_bytes_ = 0;
@@ -1643,6 +1662,38 @@ class HipComm final : public Comm {
     std::lock_guard<std::mutex> lk(tm_mu_);
     if (anchor_) event_pool_.push_back(anchor_);
     anchor_ = nullptr;
+  }
+
+ private:
+  // epoch kernels timed since the last exchange_timing(): launches, ms, remote payload bytes
+  struct XTimed {
+    hipEvent_t start, stop;
+    double remote_bytes;
+  };
+  std::vector<XTimed> xtimed_;
+  double x_launches_ = 0, x_ms_ = 0, x_remote_ = 0;
+  void reap_xtiming() {
+    for (XTimed& xt : xtimed_) {
+      HIPCHECK(hipEventSynchronize(xt.stop));
+      float ms = 0;
+      HIPCHECK(hipEventElapsedTime(&ms, xt.start, xt.stop));
+      x_launches_ += 1;
+      x_ms_ += ms;
+      x_remote_ += xt.remote_bytes;
+      std::lock_guard<std::mutex> lk(tm_mu_);
+      event_pool_.push_back(xt.start);
+      event_pool_.push_back(xt.stop);
+    }
+    xtimed_.clear();
+  }
+
+ public:
+  void exchange_timing(double out[3]) {
+    reap_xtiming();
+    out[0] = x_launches_;
+    out[1] = x_ms_;
+    out[2] = x_remote_;
+    x_launches_ = x_ms_ = x_remote_ = 0;
   }
 
  private:
@@ -1790,6 +1841,7 @@ void hip_set_stream(Comm* c, void* s) { static_cast<HipComm*>(c)->set_stream(sta
 void* hip_get_stream(Comm* c) { return static_cast<HipComm*>(c)->stream(); }
 void hip_set_timing(Comm* c, bool on) { static_cast<HipComm*>(c)->set_timing(on); }
 void hip_timing(Comm* c, double out[4]) { static_cast<HipComm*>(c)->timing(out); }
+void hip_exchange_timing(Comm* c, double out[3]) { static_cast<HipComm*>(c)->exchange_timing(out); }
 void hip_serve(Comm* c) { static_cast<HipComm*>(c)->serve(); }
 
 namespace {

@@ -60,6 +60,7 @@ SIGNATURES = [
     ("mpa_comm_payload_path", C.c_int, [_vp, C.c_int64]),
     ("mpa_comm_set_timing", C.c_int, [_vp, C.c_int]),
     ("mpa_comm_timing", C.c_int, [_vp, C.POINTER(C.c_double)]),
+    ("mpa_comm_exchange_timing", C.c_int, [_vp, C.POINTER(C.c_double)]),
     ("mpa_comm_sim_set_compute", C.c_int, [_vp, C.c_int64]),
     ("mpa_comm_sim_advance", C.c_int, [_vp, C.c_int64]),
     ("mpa_comm_sim_now", C.c_int64, [_vp]),

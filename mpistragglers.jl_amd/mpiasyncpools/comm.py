@@ -147,6 +147,13 @@ class DeviceComm(_Comm):
         check(lib().mpa_comm_timing(self._h, out))
         return int(out[0]), float(out[1]), float(out[2]), float(out[3])
 
+    def exchange_timing(self):
+        """(epoch_kernel_launches, ms, remote_payload_bytes) of the coordinator's timed epoch
+        kernels since the previous call (mpa_comm_exchange_timing)."""
+        out = (C.c_double * 3)()
+        check(lib().mpa_comm_exchange_timing(self._h, out))
+        return int(out[0]), float(out[1]), float(out[2])
+
     def aggregate(self, recvbuf, nchunks, weights, out):
         """out = sum_i weights[i] * chunk_i of recvbuf (device kernel, fixed order)."""
         w = np.ascontiguousarray(weights, dtype=np.float64)
