@@ -35,6 +35,13 @@ def test_mpi_library_exports_its_header(driver):
     names = declared([os.path.join(ROOT, "include", MPI_HEADER)])
     assert names == ["mpa_comm_create_mpi"]
     assert [n for n in names if not hasattr(lib, n)] == []
+    # before MPI_Init the transport refuses with the status / message convention of the ABI
+    h = ctypes.c_void_p()
+    lib.mpa_comm_create_mpi.argtypes = [ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]
+    assert lib.mpa_comm_create_mpi(0, ctypes.byref(h)) == 3  # MPA_ERROR
+    main = ctypes.CDLL(os.path.join(PKG, "_build", "libmpiasyncpools.so"))
+    main.mpa_last_error.restype = ctypes.c_char_p
+    assert b"MPI is not initialized" in main.mpa_last_error()
 
 
 @pytest.mark.parametrize("name", SEPARATED)
