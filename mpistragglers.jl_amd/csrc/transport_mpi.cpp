@@ -31,7 +31,7 @@ void check(int rc, const char* what) {
 
 class MpiComm final : public Comm {
  public:
-  MpiComm(MPI_Comm comm, int64_t nworkers) : Comm(nworkers), comm_(comm) {}
+  MpiComm(MPI_Comm comm, int64_t nworkers) : Comm(nworkers), comm_(comm), done_(size_t(nworkers), 0) {}
 
   ~MpiComm() override {
     // requests still in flight belong to a pool that was not drained (waitall!); cancel the
@@ -97,7 +97,6 @@ class MpiComm final : public Comm {
     const size_t k = size_t(i);
     if (posted_[k] && b_.recvbuf) std::memcpy(b_.recvbuf + k * b_.rl, posted_[k], rl_[k] < b_.rl ? rl_[k] : b_.rl);
     check(MPI_Wait(&sreq_[k], MPI_STATUS_IGNORE), "MPI_Wait");
-    done_.resize(size_t(nworkers_), 0);
     done_[size_t(rank - 1)] += 1;
   }
 
@@ -110,9 +109,7 @@ class MpiComm final : public Comm {
                         .count());
   }
 
-  int64_t tasks_done(int64_t rank) override {
-    return size_t(rank - 1) < done_.size() ? done_[size_t(rank - 1)] : 0;
-  }
+  int64_t tasks_done(int64_t rank) override { return done_[size_t(rank - 1)]; }
 
   // the worker programs own their lifecycle (the reference's examples send a control tag,
   // examples/iterative_example.jl:49-52); shutdown only refuses further posts
