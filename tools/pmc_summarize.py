@@ -45,7 +45,9 @@ def main():
     p.add_argument("--out", required=True)
     p.add_argument("--alg-bytes", type=float, required=True, help="algorithmic bytes per launch")
     p.add_argument("--skip", type=int, default=2, help="leading dispatches to drop (warm-up)")
+    p.add_argument("--kernel", default=KERNEL, help="kernel name substring")
     a = p.parse_args()
+    globals()["KERNEL"] = a.kernel
     f = per_dispatch(a.fetch, "FETCH_SIZE")[a.skip:]
     w = per_dispatch(a.write, "WRITE_SIZE")[a.skip:]
     fetch_kib, write_kib = statistics.median(f), statistics.median(w)
