@@ -107,19 +107,32 @@ def progress(msg):
     print("[bench %.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
 
 
-def gen_shard(M, torch, cfg, seed, w):
-    """Rows of worker w (1-based) of the global synthetic problem, on the current GPU
-    (b: rows; the batched variant's B: rows x 64)."""
+def gen_shards(M, torch, cfg, seed, workers):
+    """Rows of the given workers (1-based, consecutive) of the global synthetic problem on
+    the current GPU, as row-range VIEWS of one allocation per GPU (the row-sharded A of
+    BASELINE configs[1]; b: rows, the batched variant's B: rows x 64).  Measured against
+    one allocation per shard (profiles/r01_shard_alloc_ab.txt): the joint layout streams
+    c2 at a steady 7.15 TB/s where separate allocations ranged 6.6-7.25 TB/s from box to
+    box and run to run, and c5 ran 7.7 % faster; MPA_BENCH_SEPARATE=1 restores one
+    allocation per shard for that A/B."""
     n, rows, cols = cfg["workers"], cfg["rows"], cfg["cols"]
     per = rows // n
     dt = getattr(torch, TORCH_DT[cfg["dtype"]])
     k = cfg.get("iterates", 1)
-    A = torch.empty(per, cols, dtype=dt, device="cuda")
-    b = torch.empty((per, k) if k > 1 else per, dtype=dt, device="cuda")
     scale = 1.0 / np.sqrt(cols) if cfg["dtype"] == "f64" else float(np.float32(1.0 / np.sqrt(cols)))
-    M.generate(A, seed, 0, (w - 1) * per * cols, scale)
-    M.generate(b, seed, 1, (w - 1) * per * k, 1.0)
-    return A, b
+    workers = list(workers)
+    assert workers == list(range(workers[0], workers[0] + len(workers))), workers
+    if os.environ.get("MPA_BENCH_SEPARATE") == "1":
+        views = [(torch.empty(per, cols, dtype=dt, device="cuda"),
+                  torch.empty((per, k) if k > 1 else per, dtype=dt, device="cuda")) for _ in workers]
+    else:
+        A = torch.empty(per * len(workers), cols, dtype=dt, device="cuda")
+        b = torch.empty((per * len(workers), k) if k > 1 else per * len(workers), dtype=dt, device="cuda")
+        views = [(A[j * per:(j + 1) * per], b[j * per:(j + 1) * per]) for j in range(len(workers))]
+    for w, (Aw, bw) in zip(workers, views):
+        M.generate(Aw, seed, 0, (w - 1) * per * cols, scale)
+        M.generate(bw, seed, 1, (w - 1) * per * k, 1.0)
+    return views
 
 
 def delay_schedule(cfg, seed, w, count=4096):
@@ -288,7 +301,7 @@ def run_single(args, cfg):
     k = cfg.get("iterates", 1)
     batched = k > 1
     comm = M.DeviceComm(n)
-    shards = [gen_shard(M, torch, cfg, args.seed, w) for w in range(1, n + 1)]
+    shards = gen_shards(M, torch, cfg, args.seed, range(1, n + 1))
     torch.cuda.synchronize()
     progress("generated %d shards (%s)" % (n, cfg["config"]))
     for w, (A, b) in enumerate(shards, start=1):
@@ -364,12 +377,10 @@ def run_multi(args, cfg, rank, world, local):
     dist.broadcast_object_list(name, src=0)
     if rank != 0:
         comm = M.DistComm(n, placement, rank, name[0], max_msg_bytes(cfg))
-    keep = []
-    for w in range(1, n + 1):
-        if placement[w - 1] == rank:
-            A, b = gen_shard(M, torch, cfg, args.seed, w)
-            keep.append((A, b))
-            register(comm, cfg, args.seed, w, A, b)
+    mine = [w for w in range(1, n + 1) if placement[w - 1] == rank]
+    keep = gen_shards(M, torch, cfg, args.seed, mine)
+    for w, (A, b) in zip(mine, keep):
+        register(comm, cfg, args.seed, w, A, b)
     torch.cuda.synchronize()
     if rank == 0:
         progress("generated rank 0's shards (%s, %d ranks)" % (cfg["config"], world))

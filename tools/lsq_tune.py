@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--grids", default="32,48,64,96,128")
     ap.add_argument("--variants", default="2,4,5,6")
+    ap.add_argument("--separate", action="store_true",
+                    help="each worker's shard in its own allocation (as bench.py), copied from A")
     a = ap.parse_args()
     n, rows, cols = 8, 1 << 20, 1024
     per = rows // n
@@ -67,6 +69,12 @@ def main():
         nvar += 1
     variants = [int(v) for v in a.variants.split(",")] if a.variants else list(range(nvar))
     grids = [int(g) for g in a.grids.split(",")]
+    if a.separate:
+        shards = [A[(r - 1) * per:r * per].clone() for r in range(1, n + 1)]
+        del A
+        torch.cuda.empty_cache()
+    else:
+        shards = [A[(r - 1) * per:r * per] for r in range(1, n + 1)]
     isend = torch.zeros(n * cols, device="cuda")
     recv = torch.zeros(n * cols, device="cuda")
     irecv = torch.zeros_like(recv)
@@ -77,7 +85,7 @@ def main():
                 assert lib().mpa_tune(b"lsq_grid", g) == 0
                 comm = M.DeviceComm(n)
                 for r in range(1, n + 1):
-                    comm.set_task_lsq(r, A[(r - 1) * per:r * per], b[(r - 1) * per:r * per])
+                    comm.set_task_lsq(r, shards[r - 1], b[(r - 1) * per:r * per])
                 pool = M.MPIAsyncPool(n)
                 for _ in range(3):
                     M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=n)

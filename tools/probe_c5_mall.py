@@ -28,7 +28,7 @@ def main():
     cfg.update(rows=per * n, nwait=8, config="c5probe")
     torch.cuda.set_device(0)
     comm = M.DeviceComm(n)
-    shards = [bench.gen_shard(M, torch, cfg, 7, w) for w in range(1, n + 1)]
+    shards = bench.gen_shards(M, torch, cfg, 7, range(1, n + 1))
     for w, (A, b) in enumerate(shards, start=1):
         comm.set_task_lsq_batch(w, A, b)
     pool = M.MPIAsyncPool(n)
