@@ -110,10 +110,9 @@ def progress(msg):
 def gen_shards(M, torch, cfg, seed, workers):
     """Rows of the given workers (1-based, consecutive) of the global synthetic problem on
     the current GPU, as row-range VIEWS of one allocation per GPU (the row-sharded A of
-    BASELINE configs[1]; b: rows, the batched variant's B: rows x 64).  Measured against
-    one allocation per shard (profiles/r01_shard_alloc_ab.txt): the joint layout streams
-    c2 at a steady 7.15 TB/s where separate allocations ranged 6.6-7.25 TB/s from box to
-    box and run to run, and c5 ran 7.7 % faster; MPA_BENCH_SEPARATE=1 restores one
+    BASELINE configs[1]; b: rows, the batched variant's B: rows x 64).  Against one fresh
+    allocation per shard the layouts measured within run-to-run noise, the joint one the
+    steadier on c2 (profiles/r01_shard_alloc_ab.txt); MPA_BENCH_SEPARATE=1 restores one
     allocation per shard for that A/B."""
     n, rows, cols = cfg["workers"], cfg["rows"], cfg["cols"]
     per = rows // n
