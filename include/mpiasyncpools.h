@@ -22,14 +22,14 @@
  *       the `comm::MPI.Comm` argument (MPI.COMM_WORLD, examples/iterative_example.jl:8)
  *       together with the worker programs that answer on it (worker_main,
  *       examples/iterative_example.jl:55-82, test/kmap1.jl:23-33,
- *       test/kmap2.jl:110-132): a communicator whose ranks 1..n are device workers,
+ *       test/kmap2.jl:76-99): a communicator whose ranks 1..n are device workers,
  *       each running a registered task on its own HIP stream.
  *   mpa_comm_shutdown
  *       the control-tag shutdown (examples/iterative_example.jl:49-52,
- *       test/kmap2.jl:48-52)
+ *       test/kmap2.jl:14-18)
  *   mpa_aggregate / mpa_lsq_update
  *       the coordinator's consumption of `recvbuf` chunks
- *       (examples/iterative_example.jl:41-46, test/kmap2.jl:71-85) as device kernels.
+ *       (examples/iterative_example.jl:41-46, test/kmap2.jl:37-51) as device kernels.
  *
  * Status codes map onto the reference's exceptions: MPA_ARGUMENT_ERROR -> ArgumentError,
  * MPA_DIMENSION_MISMATCH -> DimensionMismatch, MPA_ERROR -> ErrorException; the message
@@ -86,7 +86,7 @@ enum mpa_task {
   MPA_TASK_NONE = 0,
   MPA_TASK_ECHO = 1,       /* reply = the received bytes (zero padded / truncated) */
   MPA_TASK_KMAP1 = 2,      /* reply = Float64(rank)            (test/kmap1.jl:24-32) */
-  MPA_TASK_KMAP2 = 3,      /* reply = Float64[rank, t, epoch]  (test/kmap2.jl:110-132) */
+  MPA_TASK_KMAP2 = 3,      /* reply = Float64[rank, t, epoch]  (test/kmap2.jl:76-99) */
   MPA_TASK_LSQ = 4,        /* reply = A_i^T (A_i x - b_i)      (BASELINE workload) */
   MPA_TASK_LSQ_BATCH = 5,  /* reply = A_i^T (A_i X - B_i), X cols x k (bf16 MFMA) */
 };

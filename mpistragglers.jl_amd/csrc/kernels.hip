@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(64) kmap_task_kernel(KmapArgs a) {
     const uint64_t m = a.sl < a.rl ? a.sl : a.rl;
     for (uint64_t j = threadIdx.x; j < a.rl; j += blockDim.x) a.out[j] = j < m ? a.x[j] : uint8_t(0);
   } else if (threadIdx.x == 0) {
-    double v[3] = {a.rank, double(a.pub.seq), 0.0};  // t == tasks served (kmap2.jl:116-118)
+    double v[3] = {a.rank, double(a.pub.seq), 0.0};  // t == tasks served (kmap2.jl:82-84)
     uint8_t* vb = reinterpret_cast<uint8_t*>(v);
     if (a.kind == MPA_TASK_KMAP2) {
       for (uint64_t j = 0; j < 8 && j < a.sl; ++j) vb[16 + j] = a.x[j];  // epoch = recvbuf[1]

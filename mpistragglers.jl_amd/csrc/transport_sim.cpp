@@ -1,5 +1,5 @@
 // SIM transport: a deterministic virtual-clock communicator whose workers run the
-// reference's test worker programs (echo, test/kmap1.jl:23-33, test/kmap2.jl:110-132) on
+// reference's test worker programs (echo, test/kmap1.jl:23-33, test/kmap2.jl:76-99) on
 // host buffers.  It exists to test the pool state machine on machines without a GPU; it
 // is never selected implicitly and carries no least-squares compute.
 //
@@ -14,7 +14,7 @@ namespace mpa {
 namespace {
 
 struct SimWorker {
-  int64_t t = 0;          // messages served (kmap2.jl:116-118)
+  int64_t t = 0;          // messages served (kmap2.jl:82-84)
   int64_t done_ns = 0;    // completion time of the outstanding task
   int64_t slot = -1;      // pool position of the outstanding request
   bool started = false;   // its send has been flushed

@@ -2,7 +2,7 @@
 
 In the reference, rank 0 of MPI.COMM_WORLD is the coordinator and ranks 1..n run a
 worker program (examples/iterative_example.jl:55-82, test/kmap1.jl:23-33,
-test/kmap2.jl:110-132).  Here a communicator owns n device workers with ranks 1..n; each
+test/kmap2.jl:76-99).  Here a communicator owns n device workers with ranks 1..n; each
 worker runs a registered task kernel on its own HIP stream:
 
     comm = DeviceComm(n)                      # HIP transport, current GPU

@@ -178,7 +178,7 @@ int orc_waitall(orc_pool* p, const orc_transport* tp,
 
 /* ---------------------------------------------------------------------------------
  * Virtual-clock worker transport.  Worker protocol restated from
- * examples/iterative_example.jl:55-82 and test/kmap2.jl:110-132: each worker serves one
+ * examples/iterative_example.jl:55-82 and test/kmap2.jl:76-99: each worker serves one
  * message at a time, replies exactly once per message, in FIFO order.  A task posted at
  * virtual time T completes at T + duration(worker, t) + compute_ns.
  * ------------------------------------------------------------------------------- */
@@ -187,7 +187,7 @@ struct orc_sim {
   int kind;
   int64_t* durations;
   int64_t now;
-  int64_t* t;          /* messages served by each worker (kmap2.jl:116-118) */
+  int64_t* t;          /* messages served by each worker (kmap2.jl:82-84) */
   int64_t* post_ns;
   int64_t* done_ns;
   int64_t* rank;
@@ -267,7 +267,7 @@ static void sim_deliver(orc_sim* s, int64_t i) {
       memcpy(out, &v, rl < 8 ? rl : 8);
       break;
     }
-    case ORC_WORKER_KMAP2: {  /* test/kmap2.jl:112-113,126-128: [rank, t, epoch] */
+    case ORC_WORKER_KMAP2: {  /* test/kmap2.jl:78-79,92-94: [rank, t, epoch] */
       double v[3];
       v[0] = (double)s->rank[i];
       v[1] = (double)s->t[i];

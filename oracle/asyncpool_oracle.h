@@ -20,7 +20,7 @@
  * Parity status: the reference is Julia + MPI.jl, neither of which exists in this
  * image, so the oracle cannot be run against the reference itself.  It is pinned by the
  * reference's own known-answer / property tests (test/kmap1.jl:22,30;
- * test/kmap2.jl:56,84,87,94,104,105), restated in tests/test_oracle.py.  MPI_Waitany
+ * test/kmap2.jl:22,50,53,60,70,71), restated in tests/test_oracle.py.  MPI_Waitany
  * tie order (several requests complete) is not pinned by any reference test: this
  * oracle defines it as lowest index first (the order MPICH's array scan returns).
  */
@@ -94,7 +94,7 @@ int orc_waitall(orc_pool* p, const orc_transport* tp,
 enum {
   ORC_WORKER_ECHO = 0,   /* reply = received bytes (truncated / zero padded) */
   ORC_WORKER_KMAP1 = 1,  /* reply[0] = Float64(rank)              test/kmap1.jl:24-32 */
-  ORC_WORKER_KMAP2 = 2,  /* reply = Float64[rank, t, epoch]        test/kmap2.jl:110-132 */
+  ORC_WORKER_KMAP2 = 2,  /* reply = Float64[rank, t, epoch]        test/kmap2.jl:76-99 */
   ORC_WORKER_TAG = 3,    /* reply = Int64[rank, t, first 8 bytes]  (trace tagging) */
 };
 

@@ -106,7 +106,7 @@ int main(int argc, char** argv) {
 
   MPI_Barrier(MPI_COMM_WORLD);  /* every worker is up before the first post */
   if (rank != 0) {
-    /* test/kmap2.jl:110-132: the worker's t-th task sleeps, then replies [rank, t, epoch] */
+    /* test/kmap2.jl:76-99: the worker's t-th task sleeps, then replies [rank, t, epoch] */
     fclose(f);
     for (int64_t t = 1;; ++t) {
       MPI_Status st;

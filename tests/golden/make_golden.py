@@ -40,7 +40,7 @@ MS = 1_000_000
 
 def predicate(name):
     """nwait::Function variants used by the scenarios."""
-    if name == "first":  # test/kmap2.jl:99
+    if name == "first":  # test/kmap2.jl:65
         return lambda epoch, repochs: bool(repochs[0] == epoch)
     if name.startswith("first_plus_"):  # BASELINE c4: worker 1 + any k others
         k = int(name.rsplit("_", 1)[1])
@@ -52,7 +52,7 @@ def predicate(name):
 
 
 def kmap2_ops(epochs=100):
-    """test/kmap2.jl:54-107: 100 epochs nwait=2, 100x (nwait=1 + waitall!), 100 epochs f."""
+    """test/kmap2.jl:20-73: 100 epochs nwait=2, 100x (nwait=1 + waitall!), 100 epochs f."""
     ops = [{"op": "asyncmap", "nwait": 2, "send": e} for e in range(1, epochs + 1)]
     for _ in range(epochs):
         ops.append({"op": "asyncmap", "nwait": 1, "send": epochs})
@@ -139,7 +139,7 @@ def scenarios():
     rng = np.random.default_rng(20261015)
     sc = []
     for n in (2, 9):  # test/runtests.jl:29-45 runs kmap2 with 3 and 10 ranks
-        # sleep(max(rand()/10, 0.005)) (test/kmap2.jl:129), microsecond resolution
+        # sleep(max(rand()/10, 0.005)) (test/kmap2.jl:95), microsecond resolution
         d = np.maximum(rng.random((n, 128)) / 10, 0.005)
         sc.append({"name": f"kmap2_n{n}", "n": n, "worker": "kmap2",
                    "durations_ns": (np.round(d * 1e6).astype(np.int64) * 1000).ravel().tolist(),

@@ -96,7 +96,7 @@ def test_kmap2(M, torch_mod, nranks):
         delay = time.perf_counter() - t0
         assert repochs[0] == pool.epoch
         assert abs(delay - pool.latency[0]) <= 1e-3
-    # t counts the tasks each worker served (kmap2.jl:116-118)
+    # t counts the tasks each worker served (kmap2.jl:82-84)
     M.waitall_(pool, recvbuf, irecvbuf)
     rb = recvbuf.cpu().numpy().reshape(nworkers, 3)
     for i in range(nworkers):
@@ -230,7 +230,7 @@ def test_lsq_padded_lda_and_determinism(M, torch_mod):
 
 def test_lsq_gradient_descent_chunks_match_their_epochs(M, torch_mod):
     """Asyncmap with least-squares workers and stragglers: each chunk i equals the
-    gradient of the iterate sent at epoch repochs[i] (kmap2.jl:84, numerically)."""
+    gradient of the iterate sent at epoch repochs[i] (kmap2.jl:50, numerically)."""
     import lsq
     torch = torch_mod
     n, rows, cols, seed = 4, 2048, 512, 11

@@ -103,7 +103,7 @@ def test_lsqb_batched_launch_counters_and_determinism(M):
 
 def test_lsqb_stragglers_chunks_match_their_epochs(M):
     """Delayed workers run the single-task path; every chunk equals G of the X of epoch
-    repochs[i] (test/kmap2.jl:84's integrity invariant, numerically)."""
+    repochs[i] (test/kmap2.jl:50's integrity invariant, numerically)."""
     import lsq
     import torch
     n, rows, cols = 3, 700, 256

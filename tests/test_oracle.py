@@ -3,8 +3,8 @@
 The reference has no golden vectors; its tests are multi-process property tests
 (test/kmap1.jl, test/kmap2.jl, run by test/runtests.jl with 3 and 10 MPI ranks).  Every
 assertion of those files is restated here against the oracle's virtual-clock workers,
-which run the same worker programs (test/kmap1.jl:23-33, test/kmap2.jl:110-132) and sleep
-the same distribution (`max(rand()/10, 0.005)` s, test/kmap2.jl:129).
+which run the same worker programs (test/kmap1.jl:23-33, test/kmap2.jl:76-99) and sleep
+the same distribution (`max(rand()/10, 0.005)` s, test/kmap2.jl:95).
 """
 import json
 import os
@@ -40,10 +40,10 @@ def test_kmap1(nranks):
 
 def _kmap2(nworkers, seed):
     rng = np.random.default_rng(seed)
-    d = np.maximum(rng.random((nworkers, 512)) / 10, 0.005)   # kmap2.jl:129
+    d = np.maximum(rng.random((nworkers, 512)) / 10, 0.005)   # kmap2.jl:95
     sim = O.OracleSim(nworkers, O.ORC_WORKER_KMAP2, (d * 1e9).astype(np.int64))
     pool = O.OraclePool(nworkers)
-    assert list(pool.ranks) == list(range(1, nworkers + 1))   # kmap2.jl:56
+    assert list(pool.ranks) == list(range(1, nworkers + 1))   # kmap2.jl:22
     sendbuf = np.empty(1)                                     # :58
     isendbuf = np.zeros(nworkers)                             # :59
     recvbuf = np.empty(3 * nworkers)                          # :60
@@ -84,7 +84,7 @@ def test_kmap2(nranks, seed):
 
 
 def test_kmap2_fifo_t_counts():
-    """The worker's message counter t (kmap2.jl:116-118) equals the tasks it served."""
+    """The worker's message counter t (kmap2.jl:82-84) equals the tasks it served."""
     pool, sim = _kmap2(9, 5)
     for i in range(9):
         assert sim.tasks(i) >= 1
@@ -172,7 +172,7 @@ def test_golden_traces_regenerate():
 
 
 def test_golden_traces_satisfy_kmap2_properties():
-    """kmap2.jl:84/:87/:94 hold on every committed trace (chunk epoch == repochs, >= nwait
+    """kmap2.jl:50/:53/:60 hold on every committed trace (chunk epoch == repochs, >= nwait
     fresh, all inactive after waitall!)."""
     ref = json.load(open(os.path.join(GOLDEN, "traces.json")))["scenarios"]
     for sc in ref:
