@@ -1,7 +1,9 @@
 """Benchmark of the asyncmap! hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1..c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+(`bench.py --gpus N` alone starts the N ranks itself, under torch.distributed.run as a child
+process, and relays rank 0's line.)
 
 One step = one coordinator epoch of the least-squares example on BASELINE configs[1] ("c2"):
     repochs = asyncmap!(pool, x, recvbuf, isendbuf, irecvbuf, comm; nwait=8)
@@ -66,7 +68,24 @@ def parse():
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dry-run", action="store_true",
+                   help="exercise the launcher, rank placement and max-over-ranks report with no GPU work "
+                        "(tests/test_bench_launch.py)")
     return p.parse_args()
+
+
+def host_cpu():
+    """(logical CPUs of the host, CPU model name) for the cpu_baseline record."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count(), model
 
 
 def cpu_baseline(cfg, seconds):
@@ -84,7 +103,9 @@ def cpu_baseline(cfg, seconds):
         r = json.loads(out.strip().splitlines()[-1])
     except Exception as e:  # report, never fake
         return {"value": None, "unit": "iterations/s", "error": str(e)[:200]}
+    host_cores, host_model = host_cpu()
     return {"value": round(r["it_per_s"], 4), "unit": "iterations/s", "cores": r["threads"], "kind": "port",
+            "threads": r["threads"], "host_cores": host_cores, "host_cpu_model": host_model,
             "sample": f"{r['epochs']} epochs in {r['seconds']:.1f} s of the full {cfg['config']} problem "
                       f"({r['workers']} worker threads + 1 coordinator thread, fp32, AVX2 loops, same state "
                       f"machine); {r['alg_GBps']:.1f} GB/s algorithmic"}
@@ -114,12 +135,14 @@ def gen_shards(M, torch, cfg, seed, workers):
     allocation per shard the layouts measured within run-to-run noise, the joint one the
     steadier on c2 (profiles/r01_shard_alloc_ab.txt); MPA_BENCH_SEPARATE=1 restores one
     allocation per shard for that A/B."""
+    workers = list(workers)
+    if not workers:  # a rank that serves no worker (c1's 3 workers over N = 4 or 8 ranks)
+        return []
     n, rows, cols = cfg["workers"], cfg["rows"], cfg["cols"]
     per = rows // n
     dt = getattr(torch, TORCH_DT[cfg["dtype"]])
     k = cfg.get("iterates", 1)
     scale = 1.0 / np.sqrt(cols) if cfg["dtype"] == "f64" else float(np.float32(1.0 / np.sqrt(cols)))
-    workers = list(workers)
     assert workers == list(range(workers[0], workers[0] + len(workers))), workers
     if os.environ.get("MPA_BENCH_SEPARATE") == "1":
         views = [(torch.empty(per, cols, dtype=dt, device="cuda"),
@@ -191,13 +214,22 @@ def report(args, cfg, world, el, per_rank, extra):
     achieved = sum(rates) / len(rates) if rates else None
     per_launch_bytes = kbytes / max(kl, 1)
     per_launch_s = kms / 1e3 / max(kl, 1)
-    traffic = None
+    # HBM traffic per launch: NOT measured in this run (PMC counters need their own
+    # rocprofv3 --pmc passes, tools/gpu_profile.sh); read from the committed summary of the
+    # same command and labelled with its file and date
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", f"lsq_pmc_{cfg['config']}.json")
     if os.path.exists(pmc) and world == 1:
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            d = json.load(open(pmc))
+            traffic = d.get("hbm_bytes_per_launch")
+            traffic_src = "%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py, %s; not this run)" % (
+                os.path.relpath(pmc, ROOT), d.get("date", "round-1 box"))
         except Exception:
             traffic = None
+    # the same kernel's average duration in the committed rocprofv3 --kernel-trace --stats
+    # summary of this command (profiles/), beside the in-process HIP-event figure
+    rocprof = rocprof_avg_ms(cfg) if world == 1 else None
     es = {"f32": 4, "f64": 8, "bf16": 2}[cfg["dtype"]]
     k = cfg.get("iterates", 1)
     epoch_bytes = es * (rows * cols + rows * k) + n * cols * k * (es + (4 if k > 1 else es))
@@ -224,18 +256,42 @@ def report(args, cfg, world, el, per_rank, extra):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                     "traffic": traffic,
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kernel_name(cfg),
                      "alg_bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4),
+                     "avg_launch_ms_source": "HIP events recorded around every launch on the stream it runs on "
+                                             "(this run, timed region only); achieved = alg bytes / busy ms",
                      "launches": kl, "busy_ms": round(sum(p[3] for p in per_rank), 3)},
         "epoch_alg_GBps": round(epoch_bytes * its / 1e9, 1),
     }
+    if rocprof:
+        out["roofline"]["rocprof_avg_launch_ms"], out["roofline"]["rocprof_source"] = rocprof
+        out["roofline"]["rocprof_frac"] = round(per_launch_bytes / (rocprof[0] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
     rp = extra.pop("measured_read_peak", None)
     if rp:
         out["roofline"]["measured_read_peak"] = rp
         out["roofline"]["frac_of_measured_read_peak"] = round(achieved / rp, 4) if achieved else None
     out.update(extra)
     return out
+
+
+ROCPROF_STATS = {"c2": ("r02_c2_kernel_stats.csv", "lsq_grad_kernel"),
+                 "c5": ("r02_c5_kernel_stats.csv", "lsqf_kernel")}
+
+
+def rocprof_avg_ms(cfg):
+    """(average ms, source) of the dominant kernel in the committed rocprofv3 --stats summary
+    of this config's bench command (profiles/), or None."""
+    name, kernel = ROCPROF_STATS.get(cfg["config"], (None, None))
+    path = os.path.join(ROOT, "profiles", name) if name else None
+    if not path or not os.path.exists(path):
+        return None
+    import csv
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Name"]:
+                return round(float(row["AverageNs"]) / 1e6, 4), "profiles/%s (%s calls)" % (name, row["Calls"])
+    return None
 
 
 def _nwait(M, cfg):
@@ -429,16 +485,81 @@ def run_multi(args, cfg, rank, world, local):
     dist.destroy_process_group()
 
 
+def run_dry(args, cfg, rank, world):
+    """--dry-run: the launcher, the rank placement, the barrier-bracketed timed region and
+    the max-over-ranks report, with the GPU work replaced by a rank-dependent sleep (CPU
+    tests of the N-process path; nothing here imports torch.cuda or the HIP library)."""
+    n = cfg["workers"]
+    placement = [(w * world) // n for w in range(n)]
+    mine = [w for w in range(1, n + 1) if placement[w - 1] == rank]
+    if os.environ.get("MPA_BENCH_DRY_FAIL_RANK") == str(rank):  # tests: a failing rank's exit code is relayed
+        raise SystemExit(3)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.002 * (1 + rank))  # the last rank is the slowest: max-over-ranks is visible
+    el = time.perf_counter() - t0
+    stats = [(el, mine)]
+    if dist is not None:
+        dist.barrier()
+        stats = [None] * world
+        dist.all_gather_object(stats, (el, mine))
+    if rank == 0:
+        el_max = max(s[0] for s in stats)
+        extra = {"dry_run": True, "placement": placement, "rank_workers": [s[1] for s in stats],
+                 "rank_elapsed_s": [round(s[0], 6) for s in stats], "cpu_baseline": None}
+        print(json.dumps(report(args, cfg, world, el_max, [(0, 0.0, 0.0, 0.0)] * world, extra)), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run the N ranks (one process
+    per GPU) under torch.distributed.run as ONE child process, started before this process
+    has touched the GPU (nothing above imports torch), relay rank 0's JSON line to stdout and
+    return the child's exit code.  The ranks' stderr passes through."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    progress("launching %d ranks: %s" % (args.gpus, " ".join(cmd[1:6])))
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    line = None
+    for out in p.stdout:
+        if out.lstrip().startswith("{"):
+            line = out.strip()
+        else:
+            sys.stderr.write(out)
+    rc = p.wait()
+    if line:
+        print(line, flush=True)
+    return rc
+
+
 def main():
     args = parse()
     cfg = dict(CONFIGS[args.config])
     cfg["config"] = args.config
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (launch N > 1 with torch.distributed.run)")
-    if world == 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        run_dry(args, cfg, rank, world)
+    elif world == 1:
         run_single(args, cfg)
     else:
         run_multi(args, cfg, rank, world, local)

@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define MPA_ABI_VERSION 1
+#define MPA_ABI_VERSION 2
 
 typedef struct mpa_pool mpa_pool;
 typedef struct mpa_comm mpa_comm;
@@ -225,9 +225,13 @@ int mpa_lsq_update(mpa_comm* comm, int dtype, void* x, const void* recvbuf, int6
  *     x  -= eta * n / sum(w) * sum_i w_i * g_i                      (mpa_lsq_update)
  * Each iteration makes exactly the calls a caller's loop makes (mpa_asyncmap, then
  * mpa_lsq_update), without an interpreter between them.  x holds cols elements; recvbuf,
- * isendbuf and irecvbuf hold n * cols. */
-int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols, void* recvbuf,
-                    void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
+ * isendbuf and irecvbuf hold n * cols, and their byte sizes are checked as asyncmap!
+ * checks them (src/MPIAsyncPools.jl:75-77: DimensionMismatch) before anything is posted.
+ * "Received" in the weights means a reply of the worker has been harvested at least once
+ * (a worker never heard from contributes nothing, whatever the pool's epoch0). */
+int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols,
+                    void* recvbuf, size_t recvbuf_bytes, void* isendbuf, size_t isendbuf_bytes,
+                    void* irecvbuf, size_t irecvbuf_bytes, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
                     void* nwait_ctx, double eta, double stale_weight, int64_t epochs);
 
 /* The batched multi-iterate variant (mpa_comm_set_task_lsq_batch): the iterate X (cols x 64)
@@ -238,8 +242,9 @@ int mpa_lsqb_update(mpa_comm* comm, void* x32, void* xb16, const void* recvbuf, 
                     const double* weights, double eta);
 /* mpa_lsq_descent for the batched variant: sendbuf = xb16 (elems bf16), recvbuf /
  * irecvbuf n * elems fp32, isendbuf n * elems bf16, update by mpa_lsqb_update. */
-int mpa_lsqb_descent(mpa_pool* pool, mpa_comm* comm, void* x32, void* xb16, int64_t elems, void* recvbuf,
-                     void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
+int mpa_lsqb_descent(mpa_pool* pool, mpa_comm* comm, void* x32, void* xb16, int64_t elems,
+                     void* recvbuf, size_t recvbuf_bytes, void* isendbuf, size_t isendbuf_bytes,
+                     void* irecvbuf, size_t irecvbuf_bytes, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
                      void* nwait_ctx, double eta, double stale_weight, int64_t epochs);
 
 /* ---- synthetic data (device): Philox4x32-10 layout of DESIGN.md §Data ------------- */

@@ -407,8 +407,9 @@ struct DescentUpdate {
 // ahead while this one's waits run (HipComm::set_ahead).  MPA_FUSE=0 runs
 // the update as its own launch after every call, MPA_AHEAD=0 disables launch-ahead.
 int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_bytes, size_t reply_es, void* recvbuf,
-                 void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
-                 void* nwait_ctx, double stale_weight, int64_t epochs, const DescentUpdate& up) {
+                 size_t recvbuf_bytes, void* isendbuf, size_t isendbuf_bytes, void* irecvbuf, size_t irecvbuf_bytes,
+                 int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn, void* nwait_ctx, double stale_weight,
+                 int64_t epochs, const DescentUpdate& up) {
   mpa::Pool& p = pool->p;
   const int64_t n = p.n;
   const int64_t elems = up.elems;
@@ -416,6 +417,19 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
   int rc = guarded([&] {
     if (!comm || !comm->c) mpa::fail(MPA_ARGUMENT_ERROR, "comm is NULL");
     need_hip(*comm->c);
+    // the buffers as the caller sized them: asyncmap!'s own checks (src/MPIAsyncPools.jl:75-77)
+    // run on these sizes, and the reply chunks must be the iterate's shape
+    if (!recvbuf || !isendbuf || !irecvbuf) mpa::fail(MPA_ARGUMENT_ERROR, "descent: recvbuf, isendbuf and irecvbuf must be given");
+    if (isendbuf_bytes != size_t(n) * msg_bytes)
+      mpa::fail(MPA_DIMENSION_MISMATCH,
+                "sendbuf is of size %zu bytes, but isendbuf is of size %zu bytes when %zu bytes are needed", msg_bytes,
+                isendbuf_bytes, size_t(n) * msg_bytes);
+    if (recvbuf_bytes != irecvbuf_bytes)
+      mpa::fail(MPA_DIMENSION_MISMATCH, "recvbuf is of size %zu bytes, but irecvbuf is of size %zu bytes", recvbuf_bytes,
+                irecvbuf_bytes);
+    if (recvbuf_bytes != size_t(n) * rl)
+      mpa::fail(MPA_DIMENSION_MISMATCH, "descent: recvbuf is of size %zu bytes, but %lld chunks of %zu bytes are needed",
+                recvbuf_bytes, (long long)n, rl);
   });
   if (rc != MPA_OK) return rc;
   mpa::Comm* c = comm->c;
@@ -438,15 +452,16 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
       });
       if (rc != MPA_OK) return rc;
     }
-    rc = mpa_asyncmap(pool, msg, msg_bytes, recvbuf, size_t(n) * rl, size_t(n * elems), isendbuf, size_t(n) * msg_bytes,
-                      irecvbuf, size_t(n) * rl, comm, nwait_kind, nwait, nwait_fn, nwait_ctx, "Int64", p.epoch + 1, 0,
+    rc = mpa_asyncmap(pool, msg, msg_bytes, recvbuf, recvbuf_bytes, recvbuf_bytes / reply_es, isendbuf, isendbuf_bytes,
+                      irecvbuf, irecvbuf_bytes, comm, nwait_kind, nwait, nwait_fn, nwait_ctx, "Int64", p.epoch + 1, 0,
                       nullptr);
     if (rc != MPA_OK) return rc;
     double sum = 0;
     for (int64_t i = 0; i < n; ++i) {
+      // fresh: weight 1; an older result: stale_weight; nothing received yet (the chunk is
+      // unfilled; test/kmap2.jl:42 skips such workers): 0
       const int64_t r = p.repochs[size_t(i)];
-      // repochs[i] == 0: nothing received yet (the convention of test/kmap2.jl:76)
-      w[size_t(i)] = r == p.epoch ? 1.0 : (r > 0 ? stale_weight : 0.0);
+      w[size_t(i)] = r == p.epoch ? 1.0 : (p.received[size_t(i)] ? stale_weight : 0.0);
       sum += w[size_t(i)];
     }
     const double s = sum > 0 ? double(n) / sum : 0.0;
@@ -473,8 +488,9 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
 }  // namespace
 extern "C" {
 
-int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols, void* recvbuf, void* isendbuf,
-                    void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn, void* nwait_ctx, double eta,
+int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t cols, void* recvbuf,
+                    size_t recvbuf_bytes, void* isendbuf, size_t isendbuf_bytes, void* irecvbuf, size_t irecvbuf_bytes,
+                    int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn, void* nwait_ctx, double eta,
                     double stale_weight, int64_t epochs) {
   int rc = guarded([&] {
     if (!pool) mpa::fail(MPA_ARGUMENT_ERROR, "pool is NULL");
@@ -483,8 +499,9 @@ int mpa_lsq_descent(mpa_pool* pool, mpa_comm* comm, int dtype, void* x, int64_t 
   });
   if (rc != MPA_OK) return rc;
   const size_t es = dtype == MPA_F64 ? 8 : 4;
-  return descent_loop(pool, comm, x, size_t(cols) * es, es, recvbuf, isendbuf, irecvbuf, nwait_kind, nwait, nwait_fn,
-                      nwait_ctx, stale_weight, epochs, DescentUpdate{dtype, cols, eta, x, nullptr, false});
+  return descent_loop(pool, comm, x, size_t(cols) * es, es, recvbuf, recvbuf_bytes, isendbuf, isendbuf_bytes, irecvbuf,
+                      irecvbuf_bytes, nwait_kind, nwait, nwait_fn, nwait_ctx, stale_weight, epochs,
+                      DescentUpdate{dtype, cols, eta, x, nullptr, false});
 }
 
 int mpa_nwait_first_plus(void* ctx, int64_t epoch, const int64_t* repochs, int64_t n) {
@@ -503,15 +520,17 @@ int mpa_lsqb_update(mpa_comm* comm, void* x32, void* xb16, const void* recvbuf, 
 }
 
 int mpa_lsqb_descent(mpa_pool* pool, mpa_comm* comm, void* x32, void* xb16, int64_t elems, void* recvbuf,
-                     void* isendbuf, void* irecvbuf, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn,
-                     void* nwait_ctx, double eta, double stale_weight, int64_t epochs) {
+                     size_t recvbuf_bytes, void* isendbuf, size_t isendbuf_bytes, void* irecvbuf,
+                     size_t irecvbuf_bytes, int nwait_kind, int64_t nwait, mpa_nwait_fn nwait_fn, void* nwait_ctx,
+                     double eta, double stale_weight, int64_t epochs) {
   int rc = guarded([&] {
     if (!pool) mpa::fail(MPA_ARGUMENT_ERROR, "pool is NULL");
     if (!x32 || !xb16 || elems <= 0 || epochs < 0) mpa::fail(MPA_ARGUMENT_ERROR, "lsqb_descent: bad arguments");
   });
   if (rc != MPA_OK) return rc;
-  return descent_loop(pool, comm, xb16, size_t(elems) * 2, 4, recvbuf, isendbuf, irecvbuf, nwait_kind, nwait, nwait_fn,
-                      nwait_ctx, stale_weight, epochs, DescentUpdate{MPA_F32, elems, eta, x32, xb16, true});
+  return descent_loop(pool, comm, xb16, size_t(elems) * 2, 4, recvbuf, recvbuf_bytes, isendbuf, isendbuf_bytes, irecvbuf,
+                      irecvbuf_bytes, nwait_kind, nwait, nwait_fn, nwait_ctx, stale_weight, epochs,
+                      DescentUpdate{MPA_F32, elems, eta, x32, xb16, true});
 }
 
 int mpa_generate(void* out, int dtype, uint64_t seed, uint32_t stream, uint64_t e0, int64_t count, double scale,

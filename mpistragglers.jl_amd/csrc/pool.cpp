@@ -7,7 +7,7 @@ namespace mpa {
 // src/MPIAsyncPools.jl:35-43, :46
 Pool::Pool(int64_t n_, const int64_t* ranks_, int64_t epoch0, int64_t nwait_)
     : n(n_), ranks(size_t(n_)), sepochs(size_t(n_), 0), repochs(size_t(n_), epoch0),
-      stimestamps(size_t(n_), 0), active(size_t(n_), 0), rreq_live(size_t(n_), 0),
+      stimestamps(size_t(n_), 0), active(size_t(n_), 0), rreq_live(size_t(n_), 0), received(size_t(n_), 0),
       latency(size_t(n_), 0.0), nwait(nwait_), epoch(epoch0) {
   for (int64_t i = 0; i < n; ++i) ranks[size_t(i)] = ranks_ ? ranks_[i] : i + 1;
 }
@@ -21,6 +21,7 @@ inline void harvest(Pool& p, Comm& c, int64_t i) {
   p.latency[k] = double(c.now_ns() - uint64_t(p.stimestamps[k])) / 1e9;
   c.harvest(i, p.ranks[k]);
   p.repochs[k] = p.sepochs[k];
+  p.received[k] = 1;
 }
 
 // isendbufs[i] .= sendbuf; sepochs; stimestamps; Isend + Irecv! (:130-138, :178-183)

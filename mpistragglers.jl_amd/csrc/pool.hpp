@@ -14,6 +14,10 @@ struct Pool {
   // never reallocated (the reference's `pool.repochs` is returned by alias, :187).
   std::vector<int64_t> ranks, sepochs, repochs, stimestamps;
   std::vector<uint8_t> active, rreq_live;
+  // received[i]: a reply of worker i has been harvested at least once (not reference state:
+  // the descent loops weight stale chunks by it; repochs[i] == epoch0 cannot tell, since an
+  // explicit epoch may equal epoch0)
+  std::vector<uint8_t> received;
   std::vector<double> latency;
   int64_t nwait = 0;
   int64_t epoch = 0;

@@ -819,8 +819,12 @@ class HipComm final : public Comm {
       for (const Harvest& h : hv)
         if (w_[size_t(h.rank - 1)].remote) remote += double(b_.rl);
       XTimed xt{};
-      xt.start = take_event();
-      xt.stop = take_event();
+      {
+        // the straggler timer thread takes events for its deferred launches too
+        std::lock_guard<std::mutex> lk(tm_mu_);
+        xt.start = take_event();
+        xt.stop = take_event();
+      }
       xt.remote_bytes = remote;
       HIPCHECK(hipEventRecord(xt.start, s));
       HIPCHECK(launch_epoch(u.dtype, a, s));
@@ -1714,6 +1718,7 @@ class HipComm final : public Comm {
       }
   }
 
+  // caller holds tm_mu_ (event_pool_ is shared with the straggler timer thread)
   hipEvent_t take_event() {
     if (!event_pool_.empty()) {
       hipEvent_t e = event_pool_.back();
@@ -1786,7 +1791,7 @@ class HipComm final : public Comm {
   UpdateSpec ahead_pred_, ahead_upd_;
   CallBufs ahead_bufs_;
   bool ahead_update_ = false;
-  bool timing_ = false;
+  std::atomic<bool> timing_{false};  // read by the straggler timer thread's launches
   bool debug_ = false;
   int arm_mode_ = 2;
   // undelayed task batches run on the coordinator stream behind the exchange that delivered

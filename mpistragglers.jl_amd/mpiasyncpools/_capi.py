@@ -6,6 +6,8 @@ There is no fallback: if the library is missing, importing the package fails lou
 import ctypes as C
 import os
 
+from . import abi
+
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # MPA_LIB: another build of the same library (A/B measurements of kernel variants)
 LIB_PATH = os.environ.get("MPA_LIB") or os.path.join(PKG_ROOT, "_build", "libmpiasyncpools.so")
@@ -19,62 +21,9 @@ MPA_NWAIT_INT, MPA_NWAIT_FN, MPA_NWAIT_OTHER = 0, 1, 2
 
 NWAIT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_int64), C.c_int64)
 
-_i64p = C.POINTER(C.c_int64)
-_vp = C.c_void_p
-_sz = C.c_size_t
-
-# (name, restype, argtypes) for every symbol declared in include/mpiasyncpools.h
-SIGNATURES = [
-    ("mpa_abi_version", C.c_int, []),
-    ("mpa_last_error", C.c_char_p, []),
-    ("mpa_build_info", C.c_char_p, []),
-    ("mpa_tune", C.c_int, [C.c_char_p, C.c_int64]),
-    ("mpa_pool_create", C.c_int, [C.c_int64, _vp, C.c_int64, C.c_int64, C.POINTER(_vp)]),
-    ("mpa_pool_destroy", None, [_vp]),
-    ("mpa_pool_size", C.c_int64, [_vp]),
-    ("mpa_pool_ranks", _i64p, [_vp]),
-    ("mpa_pool_sepochs", _i64p, [_vp]),
-    ("mpa_pool_repochs", _i64p, [_vp]),
-    ("mpa_pool_active", C.POINTER(C.c_uint8), [_vp]),
-    ("mpa_pool_stimestamps", _i64p, [_vp]),
-    ("mpa_pool_latency", C.POINTER(C.c_double), [_vp]),
-    ("mpa_pool_nwait", _i64p, [_vp]),
-    ("mpa_pool_epoch", _i64p, [_vp]),
-    ("mpa_asyncmap", C.c_int, [_vp, _vp, _sz, _vp, _sz, _sz, _vp, _sz, _vp, _sz, _vp,
-                               C.c_int, C.c_int64, _vp, _vp, C.c_char_p, C.c_int64, C.c_int64,
-                               C.POINTER(_i64p)]),
-    ("mpa_waitall", C.c_int, [_vp, _vp, _sz, _sz, _vp, _sz, C.POINTER(_i64p)]),
-    ("mpa_comm_create", C.c_int, [C.c_int, C.c_int64, _vp, C.POINTER(_vp)]),
-    ("mpa_comm_destroy", None, [_vp]),
-    ("mpa_comm_size", C.c_int64, [_vp]),
-    ("mpa_comm_set_stream", C.c_int, [_vp, _vp]),
-    ("mpa_comm_set_task_kmap", C.c_int, [_vp, C.c_int64, C.c_int]),
-    ("mpa_comm_set_task_lsq", C.c_int, [_vp, C.c_int64, C.c_int, C.c_int64, C.c_int64, _vp, C.c_int64, _vp]),
-    ("mpa_comm_set_task_lsq_batch", C.c_int, [_vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, _vp, C.c_int64, _vp]),
-    ("mpa_comm_set_delays", C.c_int, [_vp, C.c_int64, _vp, C.c_int64]),
-    ("mpa_comm_tasks_done", C.c_int64, [_vp, C.c_int64]),
-    ("mpa_comm_shutdown", C.c_int, [_vp]),
-    ("mpa_comm_create_dist", C.c_int, [C.c_int, C.c_int64, _vp, C.c_int, C.c_char_p, _sz, C.POINTER(_vp)]),
-    ("mpa_comm_serve", C.c_int, [_vp]),
-    ("mpa_comm_pause_servers", C.c_int, [_vp]),
-    ("mpa_comm_payload_path", C.c_int, [_vp, C.c_int64]),
-    ("mpa_comm_set_timing", C.c_int, [_vp, C.c_int]),
-    ("mpa_comm_timing", C.c_int, [_vp, C.POINTER(C.c_double)]),
-    ("mpa_comm_exchange_timing", C.c_int, [_vp, C.POINTER(C.c_double)]),
-    ("mpa_comm_sim_set_compute", C.c_int, [_vp, C.c_int64]),
-    ("mpa_comm_sim_advance", C.c_int, [_vp, C.c_int64]),
-    ("mpa_comm_sim_now", C.c_int64, [_vp]),
-    ("mpa_aggregate", C.c_int, [_vp, C.c_int, _vp, C.c_int64, C.c_int64, _vp, _vp]),
-    ("mpa_lsq_update", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int64, C.c_int64, _vp, C.c_double]),
-    ("mpa_lsq_descent", C.c_int, [_vp, _vp, C.c_int, _vp, C.c_int64, _vp, _vp, _vp, C.c_int, C.c_int64, _vp, _vp,
-                                  C.c_double, C.c_double, C.c_int64]),
-    ("mpa_nwait_first_plus", C.c_int, [_vp, C.c_int64, _vp, C.c_int64]),
-    ("mpa_lsqb_update", C.c_int, [_vp, _vp, _vp, _vp, C.c_int64, C.c_int64, _vp, C.c_double]),
-    ("mpa_lsqb_descent", C.c_int, [_vp, _vp, _vp, _vp, C.c_int64, _vp, _vp, _vp, C.c_int, C.c_int64, _vp, _vp,
-                                   C.c_double, C.c_double, C.c_int64]),
-    ("mpa_generate", C.c_int, [_vp, C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_int64, C.c_double, _vp]),
-    ("mpa_read_bandwidth", C.c_int, [_vp, C.c_size_t, C.c_int, C.c_int, _vp, C.POINTER(C.c_double)]),
-]
+# (name, restype, argtypes) for every symbol declared in include/mpiasyncpools.h, generated
+# from the one signature table (abi.py) the Julia binding is generated from as well
+SIGNATURES = abi.ctypes_signatures()
 
 _lib = None
 
@@ -100,7 +49,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.mpa_abi_version() != 1:
+        if L.mpa_abi_version() != abi.ABI_VERSION:
             raise ImportError("libmpiasyncpools ABI version mismatch")
         _lib = L
     return _lib

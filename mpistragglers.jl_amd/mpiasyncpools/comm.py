@@ -31,6 +31,23 @@ def dtype_code(a):
     return _DTYPES[str(a.dtype)]
 
 
+def _row_major(A, b, cols, lda):
+    """(rows, cols, lda) of a row-major A whose rows may be padded (a row-range or
+    column-slice view is fine: the leading dimension is A's row stride); b must be
+    contiguous.  A transposed view would silently give wrong gradients, so it is refused."""
+    if A.shape[0] > 1 and A.stride(1) != 1:
+        raise ArgumentError("A must be row-major with unit column stride (got strides %s)" % (tuple(A.stride()),))
+    if not b.is_contiguous():
+        raise ArgumentError("b / B must be contiguous")
+    rows = int(A.shape[0])
+    ld = int(A.stride(0)) if rows > 1 else int(A.shape[1])
+    cols = int(A.shape[1]) if cols is None else int(cols)
+    lda = ld if lda is None else int(lda)
+    if cols > lda or (rows > 1 and lda != ld):
+        raise ArgumentError(f"cols ({cols}) / lda ({lda}) do not match A's row stride ({ld})")
+    return rows, cols, lda
+
+
 class _Comm:
     transport = None
 
@@ -112,9 +129,7 @@ class DeviceComm(_Comm):
             raise ArgumentError("A must be rows x lda and b must have rows elements")
         if A.dtype != b.dtype:
             raise ArgumentError("A and b must have the same dtype")
-        rows, ld = A.shape
-        cols = ld if cols is None else int(cols)
-        lda = ld if lda is None else int(lda)
+        rows, cols, lda = _row_major(A, b, cols, lda)
         check(lib().mpa_comm_set_task_lsq(self._h, int(rank), dtype_code(A), int(rows), cols,
                                           C.c_void_p(A.data_ptr()), lda, C.c_void_p(b.data_ptr())))
         self._keep[int(rank)] = (A, b)
@@ -129,9 +144,7 @@ class DeviceComm(_Comm):
             raise ArgumentError("A must be rows x lda and B rows x k")
         if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16:
             raise ArgumentError("the batched variant takes bf16 A and B")
-        rows, ld = A.shape
-        cols = ld if cols is None else int(cols)
-        lda = ld if lda is None else int(lda)
+        rows, cols, lda = _row_major(A, B, cols, lda)
         check(lib().mpa_comm_set_task_lsq_batch(self._h, int(rank), int(rows), cols, int(B.shape[1]),
                                                 C.c_void_p(A.data_ptr()), lda, C.c_void_p(B.data_ptr())))
         self._keep[int(rank)] = (A, B)

@@ -148,7 +148,10 @@ def asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=None, epoc
     comm._before_call(sendbuf)
     err = []
     cb = None
-    if isinstance(nwait, (bool, np.bool_)):
+    fn_ptr, ctx, keep = None, None, None
+    if _is_first_plus(nwait):  # the native predicate (mpa_nwait_first_plus)
+        kind, k, fn_ptr, ctx, keep = _native_nwait(nwait)
+    elif isinstance(nwait, (bool, np.bool_)):
         kind, k = _capi.MPA_NWAIT_OTHER, 0
     elif isinstance(nwait, (int, np.integer)):
         kind, k = _capi.MPA_NWAIT_INT, int(nwait)
@@ -168,9 +171,12 @@ def asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=None, epoc
     else:
         kind, k = _capi.MPA_NWAIT_OTHER, 0
     out = C.POINTER(C.c_int64)()
+    if cb:
+        fn_ptr = C.cast(cb, C.c_void_p)
     rc = lib().mpa_asyncmap(pool._h, s_ptr, s_nb, r_ptr, r_nb, r_len, is_ptr, is_nb, ir_ptr, ir_nb,
-                            comm._h, kind, k, C.cast(cb, C.c_void_p) if cb else None, None,
-                            type(nwait).__name__.encode(), int(epoch), int(tag), C.byref(out))
+                            comm._h, kind, k, fn_ptr, ctx, type(nwait).__name__.encode(), int(epoch), int(tag),
+                            C.byref(out))
+    del keep
     if err:
         raise err[0]
     check(rc)
@@ -186,50 +192,78 @@ def waitall_(pool, recvbuf, irecvbuf):
     return pool.repochs
 
 
+def _device_buffer(name, t, dtype, numel):
+    """A contiguous CUDA tensor of `numel` elements of `dtype`: the native loops hand raw
+    pointers to device kernels, so an undersized or mistyped buffer is refused here (and its
+    byte size is checked again in the library, src/MPIAsyncPools.jl:75-77)."""
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ArgumentError(f"{name} must be a CUDA tensor")
+    if t.dtype != dtype:
+        raise ArgumentError(f"{name} must be {dtype}, but is {t.dtype}")
+    if not t.is_contiguous():
+        raise ArgumentError(f"{name} must be contiguous")
+    if t.numel() != numel:
+        raise DimensionMismatch(f"{name} has {t.numel()} elements, but {numel} are needed")
+    return C.c_void_p(t.data_ptr()), t.numel() * t.element_size()
+
+
 def lsq_descent(pool, comm, x, recvbuf, isendbuf, irecvbuf, nwait, eta, epochs, stale_weight=0.0):
     """`epochs` iterations of the least-squares coordinator loop in native code
     (mpa_lsq_descent): asyncmap_(...; nwait) then x -= eta * n/sum(w) * sum_i w_i g_i with
-    w_i = 1 for fresh chunks, stale_weight for older ones."""
+    w_i = 1 for fresh chunks, stale_weight for older ones, 0 for workers never heard from."""
     from .comm import dtype_code
-    kind, k, fn, ctx = _native_nwait(nwait)
+    n = pool.n
+    xp, _ = _device_buffer("x", x, x.dtype, x.numel())
+    r = _device_buffer("recvbuf", recvbuf, x.dtype, n * x.numel())
+    s = _device_buffer("isendbuf", isendbuf, x.dtype, n * x.numel())
+    ir = _device_buffer("irecvbuf", irecvbuf, x.dtype, n * x.numel())
+    kind, k, fn, ctx, keep = _native_nwait(nwait)
     comm._before_call(x)
-    check(lib().mpa_lsq_descent(pool._h, comm._h, dtype_code(x), C.c_void_p(x.data_ptr()), int(x.numel()),
-                                C.c_void_p(recvbuf.data_ptr()), C.c_void_p(isendbuf.data_ptr()),
-                                C.c_void_p(irecvbuf.data_ptr()), kind, k, fn, ctx,
-                                float(eta), float(stale_weight), int(epochs)))
+    check(lib().mpa_lsq_descent(pool._h, comm._h, dtype_code(x), xp, int(x.numel()), r[0], r[1], s[0], s[1],
+                                ir[0], ir[1], kind, k, fn, ctx, float(eta), float(stale_weight), int(epochs)))
+    del keep  # the predicate's context lives until the native loop has returned
     return pool.repochs
 
 
 def first_plus(k):
-    """nwait for the native loops: worker 1 fresh and >= k of the others fresh
-    (mpa_nwait_first_plus; the predicate of test/kmap2.jl:65 widened to k-of-n)."""
+    """nwait: worker 1 fresh and >= k of the others fresh (mpa_nwait_first_plus, native; the
+    predicate of test/kmap2.jl:65 widened to k-of-n).  Accepted by asyncmap_ and the native
+    loops alike."""
     return ("first_plus", int(k))
 
 
-_CTX_KEEP = []
+def _is_first_plus(nwait):
+    return isinstance(nwait, tuple) and len(nwait) == 2 and nwait[0] == "first_plus"
 
 
 def _native_nwait(nwait):
-    """(kind, int nwait, fn pointer, ctx) for the native descent loops."""
-    if isinstance(nwait, tuple) and len(nwait) == 2 and nwait[0] == "first_plus":
+    """(kind, int nwait, fn pointer, ctx pointer, keep-alive) for the native descent loops;
+    the caller holds `keep` for the duration of its call."""
+    if _is_first_plus(nwait):
         ctx = C.c_int64(nwait[1])
-        _CTX_KEEP.append(ctx)
         fn = C.cast(lib().mpa_nwait_first_plus, C.c_void_p)
-        return _capi.MPA_NWAIT_FN, 0, fn, C.cast(C.byref(ctx), C.c_void_p)
+        return _capi.MPA_NWAIT_FN, 0, fn, C.cast(C.byref(ctx), C.c_void_p), ctx
     if not isinstance(nwait, (int, np.integer)) or isinstance(nwait, bool):
         raise ArgumentError("the native loops take an integer nwait or first_plus(k)")
-    return _capi.MPA_NWAIT_INT, int(nwait), None, None
+    return _capi.MPA_NWAIT_INT, int(nwait), None, None, None
 
 
 def lsqb_descent(pool, comm, x32, xb16, recvbuf, isendbuf, irecvbuf, nwait, eta, epochs, stale_weight=0.0):
     """mpa_lsqb_descent: the coordinator loop of the batched 64-iterate variant.  x32 is the
     fp32 master iterate (cols x 64), xb16 its bf16 rounding = the message."""
-    kind, k, fn, ctx = _native_nwait(nwait)
+    import torch
+    n, e = pool.n, x32.numel()
+    x32p, _ = _device_buffer("x32", x32, torch.float32, e)
+    xbp, _ = _device_buffer("xb16", xb16, torch.bfloat16, e)
+    r = _device_buffer("recvbuf", recvbuf, torch.float32, n * e)
+    s = _device_buffer("isendbuf", isendbuf, torch.bfloat16, n * e)
+    ir = _device_buffer("irecvbuf", irecvbuf, torch.float32, n * e)
+    kind, k, fn, ctx, keep = _native_nwait(nwait)
     comm._before_call(x32)
-    check(lib().mpa_lsqb_descent(pool._h, comm._h, C.c_void_p(x32.data_ptr()), C.c_void_p(xb16.data_ptr()),
-                                 int(x32.numel()), C.c_void_p(recvbuf.data_ptr()), C.c_void_p(isendbuf.data_ptr()),
-                                 C.c_void_p(irecvbuf.data_ptr()), kind, k, fn, ctx,
-                                 float(eta), float(stale_weight), int(epochs)))
+    check(lib().mpa_lsqb_descent(pool._h, comm._h, x32p, xbp, int(e), r[0], r[1], s[0], s[1], ir[0], ir[1],
+                                 kind, k, fn, ctx, float(eta), float(stale_weight), int(epochs)))
+    del keep
     return pool.repochs
 
 

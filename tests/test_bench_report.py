@@ -59,3 +59,46 @@ def test_exchange_summary():
     assert x["launches"] == 200 and x["avg_us"] == 8.7
     assert x["remote_bytes_per_launch"] == 32768.0
     assert abs(x["remote_GBps"] - 200 * 32768.0 / 1.74e-3 / 1e9) < 1e-3
+
+
+def test_provenance_fields():
+    """the traffic figure names its source file (it is not measured in the
+    bench run), the launch time names its source, and the rocprof average of the committed
+    summary sits beside it with the fraction it implies."""
+    cfg = _cfg()
+    alg = 4299227136.0
+    out = bench.report(_args(), cfg, 1, 0.1, [(100, 60.0, 100 * alg, 60.0)], {})
+    r = out["roofline"]
+    assert "HIP events" in r["avg_launch_ms_source"]
+    if r["traffic"] is not None:
+        assert r["traffic_source"].startswith("profiles/lsq_pmc_c2.json") and "not this run" in r["traffic_source"]
+    if "rocprof_avg_launch_ms" in r:
+        ms = r["rocprof_avg_launch_ms"]
+        assert r["rocprof_source"].startswith("profiles/")
+        assert abs(r["rocprof_frac"] - alg / (ms / 1e3) / 1e9 / 8000.0) < 1e-3
+
+
+def test_cpu_baseline_records_host(monkeypatch, tmp_path):
+    """cpu_baseline: `cores` = the threads used, plus the host's logical CPU count and model."""
+    import json
+    import subprocess
+    exe = tmp_path / "cpu_baseline"
+    exe.write_text("#!/bin/sh\necho '%s'\n" % json.dumps({"it_per_s": 50.0, "threads": 9, "epochs": 600, "seconds": 12.0,
+                                                       "workers": 8, "alg_GBps": 215.0}))
+    exe.chmod(0o755)
+    real_run = subprocess.run
+    monkeypatch.setattr(bench.os.path, "exists", lambda p: True)
+    monkeypatch.setattr(bench.subprocess, "run", lambda cmd, **kw: real_run([str(exe)] + cmd[1:2], **kw))
+    cb = bench.cpu_baseline(_cfg(), 1.0)
+    assert cb["cores"] == 9 and cb["threads"] == 9 and cb["kind"] == "port"
+    assert cb["host_cores"] == os.cpu_count()
+    assert cb["host_cpu_model"] is None or isinstance(cb["host_cpu_model"], str)
+
+
+def test_gen_shards_empty_worker_list():
+    """a rank that serves no worker (c1's 3 workers on 4 or 8 ranks) gets []."""
+    assert bench.gen_shards(None, None, _cfg("c1"), 1, []) == []
+    for world in (4, 8):
+        placement = [(w * world) // 3 for w in range(3)]
+        empty = [r for r in range(world) if r not in placement]
+        assert empty  # such ranks exist and must not crash
