@@ -294,9 +294,16 @@ class HipComm final : public Comm {
         w.flag_host = &flags_[r - 1];
         w.flag_dev = &flags_[r - 1];
       }
-      if (w.here) w.stream = make_queue_stream(dev_);
     }
-    for (int k = 0; k < kLaunchStreams; ++k) launch_streams_.push_back(make_queue_stream(dev_));
+    // Worker and launch streams are created on first use (each is an HSA queue of its own):
+    // a process serving ONE pre-armed worker (N = 8) then holds one queue, not four, which
+    // matters when the GPU's hardware queue slots are shared (MPA_EAGER_STREAMS=1 restores
+    // eager creation for A/B measurements).
+    if (const char* e = std::getenv("MPA_EAGER_STREAMS"); e && *e == '1') {
+      for (auto& w : w_)
+        if (w.here) worker_stream(w);
+      launch_stream(0);
+    }
     HIPCHECK(hipEventCreateWithFlags(&xfer_ev_, hipEventDisableTiming));
     int khz = 0;
     HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
@@ -661,7 +668,7 @@ class HipComm final : public Comm {
     w.arm_tbase = w.lsqb_tbase;
     w.arm_fsbase = w.lsqf_sbase;
     w.arm_ftbase = w.lsqf_tbase;
-    HIPCHECK(hipStreamWaitValue64(w.stream, w.box_door_dev, s, hipStreamWaitValueGte, ~0ull));
+    HIPCHECK(hipStreamWaitValue64(worker_stream(w), w.box_door_dev, s, hipStreamWaitValueGte, ~0ull));
     w.seq = s;
     w.sl = task_msg_bytes(ts);
     w.rl = w.sl * (ts.kind == MPA_TASK_LSQ_BATCH ? 2 : 1);
@@ -1171,8 +1178,8 @@ class HipComm final : public Comm {
       }
       // The message is delivered now (stream-ordered after the exchange / stage-in); a
       // delayed worker "sleeps" on the host timer and only then computes.
-      if (staged) stage_in({rank}, w.stream);
-      else after_exchange(w.stream);
+      if (staged) stage_in({rank}, worker_stream(w));
+      else after_exchange(worker_stream(w));
       std::function<void()> go;
       if (ts.kind == MPA_TASK_LSQ) {
         double bytes = 0;
@@ -1331,9 +1338,22 @@ class HipComm final : public Comm {
 
   unsigned long long spin_ticks() const { return (unsigned long long)(timeout_s_ * rt_hz_); }
 
+  // the worker's own stream (delayed tasks, pre-armed tasks), created on first use
+  hipStream_t worker_stream(HipWorker& w) {
+    if (!w.stream) w.stream = make_queue_stream(dev_);
+    return w.stream;
+  }
+  // launch stream k (created on first use, up to kLaunchStreams)
+  hipStream_t launch_stream(size_t k) {
+    while (launch_streams_.size() <= k) launch_streams_.push_back(make_queue_stream(dev_));
+    return launch_streams_[k];
+  }
+
   // a launch stream with no pending work (so a batch never queues behind an unrelated
-  // straggler's kernel); round-robin if every one is busy
+  // straggler's kernel); round-robin if every one is busy; a new one while fewer than
+  // kLaunchStreams exist and all are busy
   hipStream_t pick_launch_stream() {
+    if (launch_streams_.empty()) return launch_stream(0);
     const size_t m = launch_streams_.size();
     for (size_t k = 0; k < m; ++k) {
       const size_t j = (next_launch_ + k) % m;
@@ -1342,6 +1362,7 @@ class HipComm final : public Comm {
         return launch_streams_[j];
       }
     }
+    if (m < size_t(kLaunchStreams)) return launch_stream(m);
     hipStream_t s = launch_streams_[next_launch_];
     next_launch_ = (next_launch_ + 1) % m;
     return s;
