@@ -104,10 +104,12 @@ __global__ void __launch_bounds__(kThreads) aggregate_kernel(AggregateArgs a) {
   T* out = static_cast<T*>(a.out);
   for (int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j < a.elems;
        j += int64_t(gridDim.x) * blockDim.x) {
+    // explicit fused multiply-adds: the arithmetic may not depend on how the compiler
+    // contracts the loop, so the fused epoch kernel below rounds identically
     double s = 0.0;
     for (int64_t i = 0; i < a.n; ++i)
-      if (a.w[i] != 0.0) s += a.w[i] * double(c[i * a.stride + j]);
-    const T v = a.update ? T(double(out[j]) - a.eta * s) : T(s);
+      if (a.w[i] != 0.0) s = __builtin_fma(a.w[i], double(c[i * a.stride + j]), s);
+    const T v = a.update ? T(__builtin_fma(-a.eta, s, double(out[j]))) : T(s);
     out[j] = v;
     if (a.mirror) a.mirror[j] = f32_to_bf16_rne(float(v));
   }
@@ -165,8 +167,8 @@ __global__ void __launch_bounds__(kThreads) epoch_kernel(EpochArgs a) {
         double s = 0.0;  // the fp64 sum of aggregate_kernel, in chunk order
 #pragma unroll
         for (int i = 0; i < kMaxEpochChunks; ++i)
-          if (i < a.n && a.w[i] != 0.0) s += a.w[i] * double(c[i].v[e]);
-        v.v[e] = T(double(v.v[e]) - a.eta * s);
+          if (i < a.n && a.w[i] != 0.0) s = __builtin_fma(a.w[i], double(c[i].v[e]), s);
+        v.v[e] = T(__builtin_fma(-a.eta, s, double(v.v[e])));
       }
       est<T, V>(x + j, v);
     }
