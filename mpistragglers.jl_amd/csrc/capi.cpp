@@ -2,6 +2,7 @@
 // library failures into a status code + thread-local message (mpa_last_error).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <new>
 #include <string>
@@ -434,6 +435,8 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
   if (rc != MPA_OK) return rc;
   mpa::Comm* c = comm->c;
   const bool fuse = !env_off("MPA_FUSE");
+  const char* tr = std::getenv("MPA_DESCENT_TRACE");  // repochs after every call, to stderr
+  const bool trace = tr && *tr == '1';
   const bool ahead = fuse && !env_off("MPA_AHEAD") && nwait_kind == MPA_NWAIT_INT && nwait == n;
   std::vector<double> w(static_cast<size_t>(n), 0.0);
   const std::vector<double> w_all(static_cast<size_t>(n), 1.0);  // every chunk fresh
@@ -456,6 +459,11 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
                       irecvbuf, irecvbuf_bytes, comm, nwait_kind, nwait, nwait_fn, nwait_ctx, "Int64", p.epoch + 1, 0,
                       nullptr);
     if (rc != MPA_OK) return rc;
+    if (trace) {
+      std::fprintf(stderr, "[mpa descent] epoch %lld repochs", (long long)p.epoch);
+      for (int64_t i = 0; i < n; ++i) std::fprintf(stderr, " %lld", (long long)p.repochs[size_t(i)]);
+      std::fprintf(stderr, "\n");
+    }
     double sum = 0;
     for (int64_t i = 0; i < n; ++i) {
       // fresh: weight 1; an older result: stale_weight; nothing received yet (the chunk is

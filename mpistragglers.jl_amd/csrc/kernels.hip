@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device_common.hpp"
+#include "epoch_step.hpp"
 #include "kernels.hpp"
 #include "mpiasyncpools.h"
 
@@ -93,10 +94,6 @@ __global__ void __launch_bounds__(64) kmap_task_kernel(KmapArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return uint16_t((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
-}
 
 template <typename T>
 __global__ void __launch_bounds__(kThreads) aggregate_kernel(AggregateArgs a) {
@@ -116,81 +113,12 @@ __global__ void __launch_bounds__(kThreads) aggregate_kernel(AggregateArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// The fused coordinator epoch step (EpochArgs).  Same arithmetic as aggregate_kernel (fp64
-// sum in chunk order), so the fused and unfused loops produce identical iterates.
-template <typename T, int V>
-struct EVec {
-  T v[V];
-};
-template <typename T, int V>
-__device__ __forceinline__ EVec<T, V> eld(const T* p) {
-  if constexpr (V * sizeof(T) == 16) {
-    return __builtin_bit_cast(EVec<T, V>, *reinterpret_cast<const uint4*>(p));
-  } else {
-    EVec<T, V> r;
-#pragma unroll
-    for (int e = 0; e < V; ++e) r.v[e] = p[e];
-    return r;
-  }
-}
-template <typename T, int V>
-__device__ __forceinline__ void est(T* p, const EVec<T, V>& v) {
-  if constexpr (V * sizeof(T) == 16) *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, v);
-  else
-#pragma unroll
-    for (int e = 0; e < V; ++e) p[e] = v.v[e];
-}
-
-// V elements per thread (16-B vectors when every pointer allows it).  Every chunk load is
-// issued unconditionally before any arithmetic (chunks past n read x, a valid address, and
-// are ignored): a load under a branch made the compiler wait for each one in turn.
+// The fused coordinator epoch step (EpochArgs, epoch_step.hpp): one thread per V elements,
+// then the doorbells of remote workers.  Same arithmetic as aggregate_kernel (fp64 sum in
+// chunk order), so the fused and unfused loops produce identical iterates.
 template <typename T, int V>
 __global__ void __launch_bounds__(kThreads) epoch_kernel(EpochArgs a) {
-  T* recv = reinterpret_cast<T*>(a.recv);
-  T* x = static_cast<T*>(a.x);
-  const int64_t nv = a.elems / V;
-  for (int64_t jv = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; jv < nv; jv += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t j = jv * V;
-    EVec<T, V> v = eld<T, V>(x + j);
-    EVec<T, V> c[kMaxEpochChunks];
-#pragma unroll
-    for (int i = 0; i < kMaxEpochChunks; ++i) {
-      const T* src = i < a.n ? (a.hsrc[i] ? reinterpret_cast<const T*>(a.hsrc[i]) : recv + int64_t(i) * a.elems) : x;
-      c[i] = eld<T, V>(src + j);
-    }
-#pragma unroll
-    for (int i = 0; i < kMaxEpochChunks; ++i)
-      if (i < a.n && a.hsrc[i]) est<T, V>(recv + int64_t(i) * a.elems + j, c[i]);
-    if (a.update) {
-#pragma unroll
-      for (int e = 0; e < V; ++e) {
-        double s = 0.0;  // the fp64 sum of aggregate_kernel, in chunk order
-#pragma unroll
-        for (int i = 0; i < kMaxEpochChunks; ++i)
-          if (i < a.n && a.w[i] != 0.0) s = __builtin_fma(a.w[i], double(c[i].v[e]), s);
-        v.v[e] = T(__builtin_fma(-a.eta, s, double(v.v[e])));
-      }
-      est<T, V>(x + j, v);
-    }
-    for (int i = 0; i < a.n; ++i)
-      if (a.hsrc2[i]) est<T, V>(recv + int64_t(i) * a.elems + j, eld<T, V>(reinterpret_cast<const T*>(a.hsrc2[i]) + j));
-    if (a.msg_bf16) {  // the message is the bf16 mirror (batched variant): a.mirror != NULL
-      uint16_t h[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e) h[e] = a.update ? f32_to_bf16_rne(float(v.v[e])) : a.mirror[j + e];
-#pragma unroll
-      for (int e = 0; e < V; ++e)
-        if (a.update) a.mirror[j + e] = h[e];
-      for (int d = 0; d < a.ndst; ++d)
-#pragma unroll
-        for (int e = 0; e < V; ++e) reinterpret_cast<uint16_t*>(a.dst[d])[j + e] = h[e];
-    } else {
-      if (a.update && a.mirror)
-#pragma unroll
-        for (int e = 0; e < V; ++e) a.mirror[j + e] = f32_to_bf16_rne(float(v.v[e]));
-      for (int d = 0; d < a.ndst; ++d) est<T, V>(reinterpret_cast<T*>(a.dst[d]) + j, v);
-    }
-  }
+  epoch_elems<T, V>(a, int64_t(blockIdx.x) * blockDim.x + threadIdx.x, int64_t(gridDim.x) * blockDim.x);
   if (a.ndoor == 0) return;
   // as exchange_kernel: every block's stores drained and released at system scope, then the
   // last block to arrive rings the doorbells

@@ -39,6 +39,35 @@ struct Publish {
   unsigned long long spin_ticks;  // bound on any in-kernel wait (s_memrealtime ticks)
 };
 
+// One coordinator epoch step as ONE launch (the native descent loop, DESIGN.md §5): the
+// pending harvest copies `recvbufs[i] .= irecvbufs[i]` of the previous call, the iterate
+// update x -= eta * sum_i w_i chunk_i (the user code between two asyncmap! calls,
+// examples/iterative_example.jl:41-46), the harvests of this call's phase 1, and the
+// dispatch copies `isendbufs[i] .= sendbuf` (:130) of the updated iterate, then the
+// doorbells of remote workers.  Element-parallel: element j of every chunk, of x and of
+// every message is handled by one thread, so the stages need no grid-wide ordering.
+constexpr int kMaxEpochChunks = 16;
+constexpr int kMaxEpochDst = 32;
+struct EpochArgs {
+  int64_t elems;  // elements per chunk (T) = per message
+  int n;          // chunks of recvbuf
+  int update;     // 0: no update stage (the message is x as it stands)
+  uint8_t* recv;  // recvbuf, chunk i at i * elems
+  const uint8_t* hsrc[kMaxEpochChunks];   // harvest source of chunk i before the update (NULL: none)
+  const uint8_t* hsrc2[kMaxEpochChunks];  // harvest source of chunk i after it
+  double w[kMaxEpochChunks];
+  double eta;
+  void* x;           // T[elems], updated in place
+  uint16_t* mirror;  // bf16 copy of the updated x (batched variant) or NULL
+  int msg_bf16;      // the message is the bf16 mirror (else x)
+  int ndst;
+  uint8_t* dst[kMaxEpochDst];
+  int ndoor;
+  unsigned long long* door[kMaxDoorbells];
+  unsigned long long doorval[kMaxDoorbells];
+  uint32_t* ticket;
+  uint32_t ticket_base;
+};
 // One worker task of a least-squares launch.
 struct LsqTask {
   const void* A;
@@ -73,6 +102,14 @@ struct LsqBatch {
   unsigned long long spin_ticks;
   int block0[kMaxLsqTasks + 1];
   LsqTask t[kMaxLsqTasks];
+  // Fused tail (the native descent loop at integer nwait == n): the task of
+  // this launch that completes LAST runs the NEXT epoch's coordinator step `ep` (harvest
+  // copies of this launch's replies, the iterate update, the dispatch copies of the next
+  // launch's messages; local workers only, no doorbells) in its last workgroup, so the
+  // descent loop's epoch is one launch.  tail: 0 none, 1 scalar elements, 2 16-B vectors.
+  int tail;
+  uint32_t* tail_ctr;  // task completions of this launch (the last one resets it)
+  EpochArgs ep;
 };
 // Returns hipErrorInvalidValue if no kernel variant covers (dtype, cols).
 hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s);
@@ -203,37 +240,10 @@ struct AggregateArgs {
 };
 hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s);
 
-// One coordinator epoch step as ONE launch (the native descent loop, DESIGN.md §5): the
-// pending harvest copies `recvbufs[i] .= irecvbufs[i]` of the previous call, the iterate
-// update x -= eta * sum_i w_i chunk_i (the user code between two asyncmap! calls,
-// examples/iterative_example.jl:41-46), the harvests of this call's phase 1, and the
-// dispatch copies `isendbufs[i] .= sendbuf` (:130) of the updated iterate, then the
-// doorbells of remote workers.  Element-parallel: element j of every chunk, of x and of
-// every message is handled by one thread, so the stages need no grid-wide ordering.
-constexpr int kMaxEpochChunks = 16;
-constexpr int kMaxEpochDst = 32;
-struct EpochArgs {
-  int64_t elems;  // elements per chunk (T) = per message
-  int n;          // chunks of recvbuf
-  int update;     // 0: no update stage (the message is x as it stands)
-  uint8_t* recv;  // recvbuf, chunk i at i * elems
-  const uint8_t* hsrc[kMaxEpochChunks];   // harvest source of chunk i before the update (NULL: none)
-  const uint8_t* hsrc2[kMaxEpochChunks];  // harvest source of chunk i after it
-  double w[kMaxEpochChunks];
-  double eta;
-  void* x;           // T[elems], updated in place
-  uint16_t* mirror;  // bf16 copy of the updated x (batched variant) or NULL
-  int msg_bf16;      // the message is the bf16 mirror (else x)
-  int ndst;
-  uint8_t* dst[kMaxEpochDst];
-  int ndoor;
-  unsigned long long* door[kMaxDoorbells];
-  unsigned long long doorval[kMaxDoorbells];
-  uint32_t* ticket;
-  uint32_t ticket_base;
-};
 // grid (blocks) the launch uses: the caller advances the doorbell ticket by it
 int epoch_grid(int dtype, const EpochArgs& a);
+// the step can use 16-B vectors (element count and every pointer allow it)
+bool epoch_vec(int dtype, const EpochArgs& a);
 hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s);
 
 // streaming read of `bytes` (a multiple of 16) for the measured HBM read ceiling; `sink`

@@ -34,6 +34,7 @@
 #include <cstdlib>
 
 #include "device_common.hpp"
+#include "epoch_step.hpp"
 #include "kernels.hpp"
 #include "mpiasyncpools.h"
 
@@ -377,6 +378,23 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   drain_vm();
   __syncthreads();
   if (tid == 0) publish_done(a.flag, a.seq);
+  if (!batch.tail) return;
+  // Fused tail: this workgroup finished its task (and published it); the last task of the
+  // launch to finish runs the next epoch's coordinator step.  publish_done released the
+  // reply chunk before the count; the last counter acquires the others' chunks.
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(batch.tail_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_ticket = old + 1 == unsigned(batch.ntasks);
+    if (s_ticket) {
+      __hip_atomic_store(batch.tail_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+  __syncthreads();
+  if (!s_ticket) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (batch.tail == 2) epoch_elems<T, E>(batch.ep, tid, kThreads);
+  else epoch_elems<T, 1>(batch.ep, tid, kThreads);
 }
 
 template <typename T, int VPL, int RB, int MODE>

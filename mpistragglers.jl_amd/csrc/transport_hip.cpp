@@ -263,8 +263,9 @@ class HipComm final : public Comm {
                            hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(cancel_, 0, sizeof(unsigned long long) * size_t(n + 1));
     xgmi_ = !env_off("MPA_XGMI");
-    HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 1)));
-    HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 1)));
+    // per-task tree counters, then the doorbell ticket and the fused-tail counter
+    HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 2)));
+    HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 2)));
     err_dev_ = err_;
     if (region_) {
       if (region_->nworkers() != n) fail(MPA_ARGUMENT_ERROR, "shared memory holds %lld workers, comm has %lld",
@@ -314,6 +315,7 @@ class HipComm final : public Comm {
     arm_mode_ = arm && *arm == '0' ? 0 : arm && *arm == '1' ? 1 : 2;
     const char* cb = std::getenv("MPA_COORD_BATCH");
     coord_batches_ = !(cb && *cb == '0');
+    fused_tail_ = !env_off("MPA_TAIL");
     const char* dbg = std::getenv("MPA_DEBUG");
     debug_ = dbg && *dbg == '1';
     if (debug_ && region_) {
@@ -503,7 +505,10 @@ class HipComm final : public Comm {
     return w.remote && w.path_known ? (w.path_dev ? int(kPathDevice) : int(kPathHost)) : 0;
   }
   // end_call() leaves the call's harvests pending (they join the next flush's epoch kernel)
-  void set_defer_end_flush(bool on) { defer_end_ = on; }
+  void set_defer_end_flush(bool on) {
+    defer_end_ = on;
+    if (!on) tail_next_ = tail_pending_ = false;  // the descent loop ended (or failed)
+  }
   void stage_update(const UpdateSpec& u) {
     if (ahead_update_) {  // enqueued ahead with the predicted weights: they must match
       ahead_update_ = false;
@@ -784,34 +789,28 @@ class HipComm final : public Comm {
     return ndst <= size_t(kMaxEpochDst) && ndoor <= size_t(kMaxDoorbells);
   }
 
+  // the epoch step can ride as the fused tail of the launch of `posted`: one batched
+  // least-squares launch on the coordinator stream (local, undelayed, same shape, the
+  // update's dtype), no doorbells, no bf16 mirror
+  bool tail_fits(const std::vector<int64_t>& posted, const UpdateSpec& u) const {
+    if (!fused_tail_ || posted.empty() || posted.size() > size_t(kMaxLsqTasks) || u.msg_bf16 || u.mirror) return false;
+    int cp = -1;
+    for (int64_t rank : posted) {
+      const HipWorker& w = w_[size_t(rank - 1)];
+      const TaskSpec& ts = tasks_[size_t(rank - 1)];
+      if (w.remote || ts.kind != MPA_TASK_LSQ || !ts.delays_ns.empty() || ts.dtype != u.dtype) return false;
+      const int c = lsq_cols_pad(ts.dtype, int(ts.cols));
+      if (cp >= 0 && c != cp) return false;
+      cp = c;
+    }
+    return true;
+  }
+
   // ONE epoch kernel: harvests [0, before) of `hv`, the update, harvests [before, end), the
   // dispatch copies of the posts (isendbuf slot; mailbox + doorbell for a remote worker)
   void emit_epoch(const std::vector<Harvest>& hv, size_t before, const std::vector<int64_t>& posted,
                   const UpdateSpec& u, hipStream_t s) {
-    EpochArgs a{};
-    a.elems = u.elems;
-    a.n = int(b_.n);
-    a.update = 1;
-    a.recv = b_.recvbuf;
-    for (size_t k = 0; k < hv.size(); ++k) {
-      const HipWorker& w = w_[size_t(hv[k].rank - 1)];
-      const uint8_t* src = w.remote ? reply_src(w) : b_.irecvbuf + size_t(hv[k].slot) * b_.rl;
-      (k < before ? a.hsrc : a.hsrc2)[hv[k].slot] = src;
-    }
-    for (int64_t i = 0; i < b_.n; ++i) a.w[i] = u.w[size_t(i)];
-    a.eta = u.eta;
-    a.x = u.x;
-    a.mirror = u.mirror;
-    a.msg_bf16 = u.msg_bf16 ? 1 : 0;
-    for (int64_t rank : posted) {
-      const HipWorker& w = w_[size_t(rank - 1)];
-      a.dst[a.ndst++] = b_.isendbuf + size_t(w.slot) * b_.sl;
-      if (w.remote) {
-        a.dst[a.ndst++] = msg_dst(w);
-        a.door[a.ndoor] = w.box_door_dev;
-        a.doorval[a.ndoor++] = w.seq;
-      }
-    }
+    EpochArgs a = epoch_args(hv, before, posted, u);
     if (a.ndoor > 0) {
       a.ticket = ticket_;
       a.ticket_base = ticket_count_;
@@ -842,13 +841,49 @@ class HipComm final : public Comm {
     HIPCHECK(launch_epoch(u.dtype, a, s));
   }
 
+  // the arguments of one epoch step (no doorbell ticket yet)
+  EpochArgs epoch_args(const std::vector<Harvest>& hv, size_t before, const std::vector<int64_t>& posted,
+                       const UpdateSpec& u) const {
+    EpochArgs a{};
+    a.elems = u.elems;
+    a.n = int(b_.n);
+    a.update = 1;
+    a.recv = b_.recvbuf;
+    for (size_t k = 0; k < hv.size(); ++k) {
+      const HipWorker& w = w_[size_t(hv[k].rank - 1)];
+      const uint8_t* src = w.remote ? reply_src(w) : b_.irecvbuf + size_t(hv[k].slot) * b_.rl;
+      (k < before ? a.hsrc : a.hsrc2)[hv[k].slot] = src;
+    }
+    for (int64_t i = 0; i < b_.n; ++i) a.w[i] = u.w[size_t(i)];
+    a.eta = u.eta;
+    a.x = u.x;
+    a.mirror = u.mirror;
+    a.msg_bf16 = u.msg_bf16 ? 1 : 0;
+    for (int64_t rank : posted) {
+      const HipWorker& w = w_[size_t(rank - 1)];
+      a.dst[a.ndst++] = b_.isendbuf + size_t(w.slot) * b_.sl;
+      if (w.remote) {
+        a.dst[a.ndst++] = msg_dst(w);
+        a.door[a.ndoor] = w.box_door_dev;
+        a.doorval[a.ndoor++] = w.seq;
+      }
+    }
+    return a;
+  }
+
   // enqueue the next epoch of an await-all call (set_ahead), once per call, when this
   // call has posted every worker of the pool
   void maybe_ahead() {
-    if (ahead_left_ <= 0 || !b_.await_all || int64_t(call_posts_.size()) != b_.n) return;
+    // an ahead epoch whose step already ran in the previous launch's fused tail must be
+    // enqueued now: the descent loop that set it up guarantees it (anything else would apply
+    // that update twice)
+    auto skip = [this]() {
+      if (tail_pending_) fail(MPA_ERROR, "fused tail: the epoch it prepared was not enqueued ahead");
+    };
+    if (ahead_left_ <= 0 || !b_.await_all || int64_t(call_posts_.size()) != b_.n) return skip();
     UpdateSpec& u = ahead_pred_;
     for (const auto& cp : call_posts_)
-      if (w_[size_t(cp.rank - 1)].preposted) return;
+      if (w_[size_t(cp.rank - 1)].preposted) return skip();
     // the next epoch's posts equal this call's: same slots, same buffers; only workers
     // whose task starts as soon as its message lands (no injected delay, whose sleep
     // begins at delivery on the host timer)
@@ -856,10 +891,11 @@ class HipComm final : public Comm {
     for (const auto& cp : call_posts_) {
       const HipWorker& w = w_[size_t(cp.rank - 1)];
       const TaskSpec& ts = tasks_[size_t(cp.rank - 1)];
-      if (!w.remote && ((ts.kind != MPA_TASK_LSQ && ts.kind != MPA_TASK_LSQ_BATCH) || !ts.delays_ns.empty())) return;
+      if (!w.remote && ((ts.kind != MPA_TASK_LSQ && ts.kind != MPA_TASK_LSQ_BATCH) || !ts.delays_ns.empty())) return skip();
       posted.push_back(cp.rank);
     }
-    if (!fused_ok(u, posted)) return;
+    if (!fused_ok(u, posted)) return skip();
+    const bool more = ahead_left_ >= 2;  // the call after next enqueues another ahead epoch
     ahead_left_ = 0;
     // the replies of this call's remote tasks must have landed before the epoch kernel
     // reads them (local tasks are stream-ordered before it on the coordinator stream)
@@ -871,8 +907,19 @@ class HipComm final : public Comm {
       hv.push_back({cp.slot, cp.rank});
     }
     for (int64_t rank : posted) w_[size_t(rank - 1)].seq += 1;  // the ahead epoch's task numbers
-    emit_epoch(hv, hv.size(), posted, u, coord_);
+    if (tail_pending_) tail_pending_ = false;  // this step ran in the previous launch's tail
+    else emit_epoch(hv, hv.size(), posted, u, coord_);
+    // Fused tail: at nwait == n every epoch's step is the same (harvest all n, weight 1 each,
+    // re-post all n), so when another ahead epoch follows, THIS epoch's launch runs the next
+    // step in its last workgroup and the next maybe_ahead enqueues only the launch
+    if (more && tail_fits(posted, u)) {
+      tail_args_ = epoch_args(hv, hv.size(), posted, u);
+      tail_ranks_ = posted.size();
+      tail_next_ = true;
+      tail_pending_ = true;
+    }
     launch_local(posted);
+    if (tail_next_) fail(MPA_ERROR, "fused tail: no least-squares launch took it");
     for (int64_t rank : posted) {
       HipWorker& w = w_[size_t(rank - 1)];
       w.seq -= 1;  // the pool's view: its next post() takes the enqueued number
@@ -1370,7 +1417,15 @@ class HipComm final : public Comm {
 
   void launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hipStream_t s) {
     double bytes = 0;
-    const LsqBatch b = build_lsq_batch(ranks, dtype, &bytes);
+    LsqBatch b = build_lsq_batch(ranks, dtype, &bytes);
+    if (tail_next_) {  // maybe_ahead: this launch runs the next epoch's step (fused tail)
+      if (s != coord_ || ranks.size() != tail_ranks_)
+        fail(MPA_ERROR, "fused tail: the launch does not cover the epoch's %zu workers", tail_ranks_);
+      b.tail = epoch_vec(dtype, tail_args_) ? 2 : 1;
+      b.tail_ctr = tail_ctr_;
+      b.ep = tail_args_;
+      tail_next_ = false;
+    }
     enqueue_lsq(b, dtype, int(tasks_[size_t(ranks[0] - 1)].cols), s, bytes);
   }
 
@@ -1797,6 +1852,13 @@ class HipComm final : public Comm {
   uint32_t* ctr_ = nullptr;
   uint32_t* ticket_ = nullptr;
   uint32_t ticket_count_ = 0;
+  // fused tail (maybe_ahead): the next least-squares launch carries tail_args_ (tail_next_);
+  // the epoch step of the next ahead epoch is already enqueued in a tail (tail_pending_)
+  uint32_t* tail_ctr_ = nullptr;
+  bool fused_tail_ = true;  // MPA_TAIL=0: a separate epoch kernel every epoch
+  bool tail_next_ = false, tail_pending_ = false;
+  size_t tail_ranks_ = 0;
+  EpochArgs tail_args_{};
   hipEvent_t xfer_ev_ = nullptr;
   double rt_hz_ = 100e6;
   double timeout_s_ = 600.0;
@@ -1839,7 +1901,10 @@ class HipComm final : public Comm {
   std::string tfail_msg_;
 
  public:
-  void init_ticket() { ticket_ = ctr_ + kLsqCtrPerTask * nworkers_; }
+  void init_ticket() {
+    ticket_ = ctr_ + kLsqCtrPerTask * nworkers_;
+    tail_ctr_ = ticket_ + 1;
+  }
 };
 
 }  // namespace

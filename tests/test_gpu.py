@@ -335,11 +335,12 @@ def test_full_size_c2_against_torch_fp64(M, torch_mod):
     assert torch.equal(isend.view(n, cols), x.expand(n, cols))
 
 
-@pytest.mark.parametrize("env", [{}, {"MPA_AHEAD": "0"}, {"MPA_FUSE": "0"}])
+@pytest.mark.parametrize("env", [{}, {"MPA_TAIL": "0"}, {"MPA_AHEAD": "0"}, {"MPA_FUSE": "0"}])
 def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod, monkeypatch, env):
     """mpa_lsq_descent makes the same calls as the Python loop: identical iterates (bitwise,
-    nwait = n so every epoch is fresh and every kernel is deterministic), with the fused
-    epoch kernel and launch-ahead (default), fused only, and unfused."""
+    nwait = n so every epoch is fresh and every kernel is deterministic), with launch-ahead
+    and the epoch step fused into the previous launch's tail (default), launch-ahead with a
+    separate epoch kernel, the fused epoch kernel only, and unfused."""
     import lsq
     torch = torch_mod
     for k, v in env.items():
@@ -358,7 +359,16 @@ def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod, monkeypatch, 
         recv = torch.zeros(n * cols, device="cuda")
         irecv = torch.zeros_like(recv)
         if native:
+            comm.set_timing(True)
             M.lsq_descent(pool, comm, x, recv, isend, irecv, n, 0.01, 6)
+            xl = comm.exchange_timing()[0]
+            comm.set_timing(False)
+            # epoch kernels: with the fused tail only the first ahead step (update 1) and the
+            # final update (6) run as their own launches; updates 2-5 ride in launch tails
+            if not env:
+                assert xl == 2, xl
+            elif env == {"MPA_TAIL": "0"}:
+                assert xl == 6, xl
         else:
             for _ in range(6):
                 rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=n)
