@@ -462,6 +462,10 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
     if (trace) {
       std::fprintf(stderr, "[mpa descent] epoch %lld repochs", (long long)p.epoch);
       for (int64_t i = 0; i < n; ++i) std::fprintf(stderr, " %lld", (long long)p.repochs[size_t(i)]);
+      std::fprintf(stderr, " | sepochs");
+      for (int64_t i = 0; i < n; ++i) std::fprintf(stderr, " %lld", (long long)p.sepochs[size_t(i)]);
+      std::fprintf(stderr, " | latency ms");
+      for (int64_t i = 0; i < n; ++i) std::fprintf(stderr, " %.1f", p.latency[size_t(i)] * 1e3);
       std::fprintf(stderr, "\n");
     }
     double sum = 0;

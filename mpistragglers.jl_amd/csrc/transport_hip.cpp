@@ -296,14 +296,22 @@ class HipComm final : public Comm {
         w.flag_dev = &flags_[r - 1];
       }
     }
-    // Worker and launch streams are created on first use (each is an HSA queue of its own):
-    // a process serving ONE pre-armed worker (N = 8) then holds one queue, not four, which
-    // matters when the GPU's hardware queue slots are shared (MPA_EAGER_STREAMS=1 restores
-    // eager creation for A/B measurements).
-    if (const char* e = std::getenv("MPA_EAGER_STREAMS"); e && *e == '1') {
+    // Streams are HSA queues of their own, and creating one takes milliseconds, so none is
+    // created inside a timed schedule: a worker's stream when its task is registered
+    // (on_task_changed), the launch streams here where they can be used (a worker process
+    // serving several workers batches staged tasks on them).  A process serving ONE
+    // pre-armed worker (N = 8) then holds one queue, not four, which matters when the
+    // GPU's hardware queue slots are shared; MPA_EAGER_STREAMS=1 creates every stream up
+    // front (the round-1 behaviour, for A/B measurements).
+    int here_count = 0;
+    for (const auto& w : w_) here_count += w.here;
+    const char* eager = std::getenv("MPA_EAGER_STREAMS");
+    if (eager && *eager == '1') {
       for (auto& w : w_)
         if (w.here) worker_stream(w);
-      launch_stream(0);
+      launch_stream(kLaunchStreams - 1);
+    } else if (role_ == SERVER && here_count > 1) {
+      launch_stream(kLaunchStreams - 1);
     }
     HIPCHECK(hipEventCreateWithFlags(&xfer_ev_, hipEventDisableTiming));
     int khz = 0;
@@ -564,6 +572,7 @@ class HipComm final : public Comm {
       fail(MPA_ARGUMENT_ERROR, "worker %lld is served by another process; register its task there", (long long)rank);
     if (w.seq != uint64_t(tasks_done(rank)))
       fail(MPA_ERROR, "cannot change the task of worker %lld while it has an outstanding request", (long long)rank);
+    worker_stream(w);  // outside any timed schedule (delayed and pre-armed tasks run on it)
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
     if (ts.kind == MPA_TASK_LSQ) prepare_lsq(rank, ts);
     if (ts.kind == MPA_TASK_LSQ_BATCH) prepare_lsqb(rank, ts);
