@@ -11,6 +11,10 @@
 #include "kernels.hpp"
 #include "pool.hpp"
 
+#ifndef MPA_MEASURE
+#define MPA_MEASURE 0
+#endif
+
 namespace mpa {
 void sim_set_compute(Comm* c, int64_t ns);
 void sim_advance(Comm* c, int64_t dt);
@@ -99,7 +103,8 @@ int mpa_tune(const char* key, int64_t value) {
 }
 
 const char* mpa_build_info(void) {
-  static std::string info = std::string("gfx950; lsq c2 variant: ") + mpa::lsq_variant_name();
+  static std::string info = std::string("gfx950; lsq c2 variant: ") + mpa::lsq_variant_name() +
+                            (MPA_MEASURE ? "; measurement build (MEASURE=1)" : "");
   return info.c_str();
 }
 

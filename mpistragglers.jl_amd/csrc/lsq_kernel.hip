@@ -18,7 +18,8 @@
 // last one writes the reply chunk and publishes completion.  Nothing waits on another
 // workgroup, so the result never depends on how many workgroups are resident.
 //
-// Compile-time variants (MODE bits) exist for measurement (DESIGN.md §Kernel tuning):
+// Compile-time variants (MODE bits) exist for measurement (DESIGN.md §Kernel tuning; all of
+// them are compiled only into the measurement build, make MEASURE=1):
 //   M_CLAMP     branch-free loads: out-of-range rows/vectors read a clamped in-bounds
 //               address and are multiplied by zero instead of branched around
 //   M_DPP       wave reduction by DPP row ops + readlane instead of ds_bpermute
@@ -32,6 +33,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+
+#ifndef MPA_MEASURE
+#define MPA_MEASURE 0
+#endif
 
 #include "device_common.hpp"
 #include "epoch_step.hpp"
@@ -420,12 +425,15 @@ struct Variant {
   const char* name;
 };
 constexpr Variant kC2Variants[] = {
+    // shipped: 6.5 TB/s on c2 in the round-1 sweep (profiles/r01_tune_sweep*.jsonl)
+    {go<float, 4, 4, M_CLAMP | M_DPP | M_NT>, 4, "rb4+clamp+dpp+nt"},
+#if MPA_MEASURE
+    // the tuning space of that sweep (measurement build only: make MEASURE=1)
     {go<float, 4, 4, 0>, 4, "rb4"},
     {go<float, 4, 4, M_CLAMP>, 4, "rb4+clamp"},
     {go<float, 4, 4, M_CLAMP | M_DPP>, 4, "rb4+clamp+dpp"},
     {go<float, 4, 2, M_CLAMP | M_DPP | M_PREFETCH>, 2, "rb2+clamp+dpp+prefetch"},
     {go<float, 4, 4, M_CLAMP | M_DPP | M_PREFETCH>, 4, "rb4+clamp+dpp+prefetch"},
-    {go<float, 4, 4, M_CLAMP | M_DPP | M_NT>, 4, "rb4+clamp+dpp+nt"},
     {go<float, 4, 2, M_CLAMP | M_DPP | M_PREFETCH | M_NT>, 2, "rb2+clamp+dpp+prefetch+nt"},
     {go<float, 4, 8, M_CLAMP | M_DPP>, 8, "rb8+clamp+dpp"},
     {go<float, 4, 2, M_CLAMP | M_DPP>, 2, "rb2+clamp+dpp"},
@@ -434,9 +442,10 @@ constexpr Variant kC2Variants[] = {
     {go<float, 4, 2, M_CLAMP | M_DPP | M_PREFETCH | M_NT | M_BLOCKED>, 2, "rb2+clamp+dpp+prefetch+nt+blocked"},
     {go<float, 4, 4, M_CLAMP | M_DPP | M_PREFETCH | M_NT | M_BLOCKED>, 4, "rb4+clamp+dpp+prefetch+nt+blocked"},
     {go<float, 4, 8, M_CLAMP | M_DPP | M_NT | M_BLOCKED>, 8, "rb8+clamp+dpp+nt+blocked"},
+#endif
 };
 constexpr int kNumC2Variants = int(sizeof(kC2Variants) / sizeof(kC2Variants[0]));
-constexpr int kDefaultC2 = 5;  // rb4+clamp+dpp+nt: 6.5 TB/s on c2 (profiles/r01_tune.txt)
+constexpr int kDefaultC2 = 0;
 
 int g_variant = -1;  // set by MPA_LSQ_VARIANT or mpa_tune("lsq_variant", i)
 

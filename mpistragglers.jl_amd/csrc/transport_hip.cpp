@@ -44,6 +44,10 @@
 #include "kernels.hpp"
 #include "shm.hpp"
 
+#ifndef MPA_MEASURE
+#define MPA_MEASURE 0
+#endif
+
 namespace mpa {
 
 #define HIPCHECK(expr)                                                                  \
@@ -341,7 +345,7 @@ class HipComm final : public Comm {
     }
     stop_timer();
     (void)hipDeviceSynchronize();
-    if (const char* d = std::getenv("MPA_LSQF_DBG"); d && (std::atoi(d) & 16)) lsqf_prof_dump();
+    if (const char* d = MPA_MEASURE ? std::getenv("MPA_LSQF_DBG") : nullptr; d && (std::atoi(d) & 16)) lsqf_prof_dump();
     for (auto& w : w_) {
       if (w.slab) (void)hipFree(w.slab);
       if (w.lsqb_R) (void)hipFree(w.lsqb_R);
@@ -1500,6 +1504,7 @@ class HipComm final : public Comm {
 
   // the iterate-quarter single pass (lsqq_kernel.hip): cols <= 2048 on every task
   bool lsqq_enabled(const std::vector<int64_t>& ranks) const {
+    if (!MPA_MEASURE) return false;  // a probe kernel of the measurement build (make MEASURE=1)
     const char* e = std::getenv("MPA_LSQQ");
     if (!e || *e != '1') return false;
     for (int64_t rank : ranks) {
@@ -1576,8 +1581,9 @@ class HipComm final : public Comm {
       b.ntasks = int(ranks.size());
       b.err = err_dev_;
       b.spin_ticks = spin_ticks();
-      { const char* d = std::getenv("MPA_LSQF_DBG"); b.dbg = d ? std::atoi(d) : 0; }
-      { const char* d = std::getenv("MPA_LSQF_LAG"); b.lag = d ? std::atoi(d) : 4; }
+      // probe modes and the phase-1 lead: measurement build only (make MEASURE=1)
+      { const char* d = MPA_MEASURE ? std::getenv("MPA_LSQF_DBG") : nullptr; b.dbg = d ? std::atoi(d) : 0; }
+      { const char* d = MPA_MEASURE ? std::getenv("MPA_LSQF_LAG") : nullptr; b.lag = d ? std::atoi(d) : 4; }
       b.P = int((tasks_[size_t(ranks[0] - 1)].cols + kLsqfSlice - 1) / kLsqfSlice);
       // one workgroup per CU: groups of P, as many as keep the grid a multiple of 8 P (the
       // groups form inside an XCD, 8 XCDs), dealt evenly over the tasks
@@ -1676,7 +1682,11 @@ class HipComm final : public Comm {
       tl.rank = armed_rank;
       HIPCHECK(hipEventRecord(tl.start, s));
     }
+#if MPA_MEASURE
     HIPCHECK(b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
+#else
+    HIPCHECK(b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
+#endif
     if (timed) {
       HIPCHECK(hipEventRecord(tl.stop, s));
       std::lock_guard<std::mutex> lk(tm_mu_);
