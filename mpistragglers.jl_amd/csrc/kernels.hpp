@@ -155,6 +155,34 @@ struct LsqbBatch {
 // pass 1 + pass 2 of every task of the batch, two launches on `s`
 hipError_t launch_lsqb(const LsqbBatch& a, hipStream_t s);
 
+// Single pass by iterate halves (lsqp_kernel.hip, the c5 default for cols <= 2048): pairs of
+// workgroups stream the same rows, member h owning iterates 32h .. 32h + 31 of R and G; no
+// exchange between members.  Pairs [grp0[t], grp0[t+1]) serve task t (grid = 16 x ceil(pairs
+// / 8): the members of pair p are blocks 16 (p / 8) + p % 8 and that + 8).
+constexpr int kLsqpMaxGroups = 128;   // pairs (row groups) per task
+constexpr int kLsqpCtrPerSlice = 64;  // tree counters per (half, wave): 32 + 8 + 2 + 1, rounded up
+constexpr int kLsqpMaxCols = 2048;    // 8 waves x 256 columns
+struct LsqpTask {
+  const void* A;
+  const void* B;
+  const void* X;
+  void* out;
+  void* slab;      // [2][kLsqpMaxGroups][8 waves][32 KiB] fp32 G partials (tree reduced in place)
+  uint32_t* ctr;   // [2 halves][8 waves][kLsqpCtrPerSlice] tree counters + [1] slice completions;
+                   // every counter is reset by its last arriver
+  unsigned long long* flag;
+  unsigned long long seq;
+  int64_t rows, lda;
+  int cols;
+  const unsigned long long* go;  // as LsqTask::go
+};
+struct LsqpBatch {
+  int ntasks;
+  int grp0[kMaxLsqTasks + 1];
+  LsqpTask t[kMaxLsqTasks];
+};
+hipError_t launch_lsqp(const LsqpBatch& a, hipStream_t s);
+
 // Single-pass variant (lsqf_kernel.hip): groups of P = ceil(cols / kLsqfSlice) workgroups,
 // one 512-column slice each, exchanging per-block partial residuals through `xbuf`.
 constexpr int kLsqfSlice = 512;

@@ -154,6 +154,9 @@ struct HipWorker {
   unsigned long long* lsqf_flag = nullptr;
   uint32_t* lsqf_ctr = nullptr;
   uint32_t* lsqq_ctr = nullptr;  // quad kernel: [4] member arrivals, [4] completions (self-resetting)
+  // pair single pass (lsqp_kernel.hip): G partials and tree counters (self-resetting)
+  void* lsqp_slab = nullptr;
+  uint32_t* lsqp_ctr = nullptr;
   uint32_t lsqf_sbase = 0, lsqf_tbase = 0;
   // current task
   int64_t slot = -1;
@@ -355,6 +358,8 @@ class HipComm final : public Comm {
       if (w.lsqf_flag) (void)hipFree(w.lsqf_flag);
       if (w.lsqf_ctr) (void)hipFree(w.lsqf_ctr);
       if (w.lsqq_ctr) (void)hipFree(w.lsqq_ctr);
+      if (w.lsqp_slab) (void)hipFree(w.lsqp_slab);
+      if (w.lsqp_ctr) (void)hipFree(w.lsqp_ctr);
       if (w.peer_msg) (void)hipIpcCloseMemHandle(w.peer_msg);
       if (w.peer_reply) (void)hipIpcCloseMemHandle(w.peer_reply);
       if (w.xslot) (void)hipFree(w.xslot);
@@ -1163,6 +1168,13 @@ class HipComm final : public Comm {
       HIPCHECK(hipMemset(w.lsqb_ctr, 0, sizeof(uint32_t) * (kLsqbMaxSlices + 1)));
       HIPCHECK(hipDeviceSynchronize());
     }
+    if (ts.cols <= kLsqpMaxCols && !w.lsqp_slab) {
+      HIPCHECK(hipMalloc(&w.lsqp_slab, size_t(2) * kLsqpMaxGroups * 8 * 32 * 1024));
+      const size_t nctr = size_t(2) * 8 * kLsqpCtrPerSlice + 1;
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqp_ctr), sizeof(uint32_t) * nctr));
+      HIPCHECK(hipMemset(w.lsqp_ctr, 0, sizeof(uint32_t) * nctr));
+      HIPCHECK(hipDeviceSynchronize());
+    }
     if (ts.cols <= 2048 && !w.lsqq_ctr) {
       HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqq_ctr), sizeof(uint32_t) * 8));
       HIPCHECK(hipMemset(w.lsqq_ctr, 0, sizeof(uint32_t) * 8));
@@ -1490,17 +1502,31 @@ class HipComm final : public Comm {
   // task of the batch has the same slice count (cols <= 2048) and MPA_LSQF is not 0, else
   // the two passes (lsqb_kernel.hip).
   struct LsqbLaunch {
+    bool pair = false;   // lsqp (the default single pass)
     bool fused = false;  // lsqf (opt-in)
     bool quad = false;   // lsqq
     LsqbBatch two{};
     LsqfBatch one{};
     LsqqBatch four{};
+    LsqpBatch halves{};
     void set_go(const unsigned long long* go) {
-      if (quad) four.t[0].go = go;
+      if (pair) halves.t[0].go = go;
+      else if (quad) four.t[0].go = go;
       else if (fused) one.t[0].go = go;
       else two.t[0].go = go;
     }
   };
+
+  // the iterate-halves single pass (lsqp_kernel.hip): the default for cols <= 2048
+  // (MPA_LSQP=0 selects the two passes)
+  bool lsqp_enabled(const std::vector<int64_t>& ranks) const {
+    if (env_off("MPA_LSQP")) return false;
+    for (int64_t rank : ranks) {
+      const TaskSpec& ts = tasks_[size_t(rank - 1)];
+      if (!w_[size_t(rank - 1)].lsqp_slab || ts.cols > kLsqpMaxCols) return false;
+    }
+    return !ranks.empty();
+  }
 
   // the iterate-quarter single pass (lsqq_kernel.hip): cols <= 2048 on every task
   bool lsqq_enabled(const std::vector<int64_t>& ranks) const {
@@ -1541,6 +1567,38 @@ class HipComm final : public Comm {
                2.0 * double(ts.cols) * double(ts.k) + 4.0 * double(ts.cols) * double(ts.k);
     }
     *bytes_out = bytes;
+    if (lsqp_enabled(ranks) && !lsqf_enabled(ranks) && !lsqq_enabled(ranks)) {
+      L.pair = true;
+      LsqpBatch& b = L.halves;
+      b.ntasks = int(ranks.size());
+      // one workgroup per CU: 128 pairs (256 workgroups), dealt evenly over the tasks
+      constexpr int target = 128;
+      int pairs = 0;
+      for (int k = 0; k < b.ntasks; ++k) {
+        const int64_t rank = ranks[size_t(k)];
+        HipWorker& w = w_[size_t(rank - 1)];
+        const TaskSpec& ts = tasks_[size_t(rank - 1)];
+        LsqpTask& t = b.t[k];
+        t.A = ts.A;
+        t.B = ts.b;
+        t.X = w.x;
+        t.out = w.out;
+        t.slab = w.lsqp_slab;
+        t.ctr = w.lsqp_ctr;
+        t.flag = w.flag_dev;
+        t.seq = w.seq;
+        t.rows = ts.rows;
+        t.lda = ts.lda;
+        t.cols = int(ts.cols);
+        const int per = target / b.ntasks + (k < target % b.ntasks ? 1 : 0);
+        const int64_t nblocks = (ts.rows + 15) / 16;
+        const int ng = int(std::max<int64_t>(1, std::min<int64_t>(std::min(per, kLsqpMaxGroups), nblocks)));
+        b.grp0[k] = pairs;
+        pairs += ng;
+      }
+      b.grp0[b.ntasks] = pairs;
+      return L;
+    }
     if (lsqq_enabled(ranks)) {
       L.quad = true;
       LsqqBatch& b = L.four;
@@ -1683,9 +1741,9 @@ class HipComm final : public Comm {
       HIPCHECK(hipEventRecord(tl.start, s));
     }
 #if MPA_MEASURE
-    HIPCHECK(b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
+    HIPCHECK(b.pair ? launch_lsqp(b.halves, s) : b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #else
-    HIPCHECK(b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
+    HIPCHECK(b.pair ? launch_lsqp(b.halves, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #endif
     if (timed) {
       HIPCHECK(hipEventRecord(tl.stop, s));
