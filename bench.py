@@ -168,6 +168,8 @@ def delay_schedule(cfg, seed, w, count=4096):
 
 def kernel_name(cfg):
     if cfg.get("iterates", 1) > 1:
+        if os.environ.get("MPA_LSQP", "1") != "0" and cfg["cols"] <= 2048:
+            return "lsqp_kernel (bf16 MFMA single pass by iterate halves, one launch per batch)"
         return "lsqb_resid_kernel + lsqb_grad_kernel (bf16 MFMA, two launches per batch)"
     return "lsq_grad_kernel (one batched launch per epoch per GPU)"
 
@@ -276,7 +278,7 @@ def report(args, cfg, world, el, per_rank, extra):
 
 
 ROCPROF_STATS = {"c2": ("r02_c2_kernel_stats.csv", "lsq_grad_kernel"),
-                 "c5": ("r02_c5_kernel_stats.csv", "lsqf_kernel")}
+                 "c5": ("r02_c5_kernel_stats.csv", "lsqp_kernel")}
 
 
 def rocprof_avg_ms(cfg):

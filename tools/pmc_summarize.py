@@ -15,6 +15,7 @@ import glob
 import json
 import os
 import statistics
+import time
 
 KERNEL = "lsq_grad_kernel"
 
@@ -63,6 +64,7 @@ def main():
         "hbm_bytes_per_launch": read_b + write_b,
         "alg_bytes_per_launch": a.alg_bytes,
         "traffic_over_alg": (read_b + write_b) / a.alg_bytes,
+        "date": time.strftime("%Y-%m-%d"),
         "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes",
     }
     with open(a.out, "w") as fh:
