@@ -178,10 +178,14 @@ struct LsqpTask {
 };
 struct LsqpBatch {
   int ntasks;
+  int pfd;  // L2 prefetch lead over the LDS-DMA, in blocks (0: none); MPA_LSQP_PF
+  int dbg;  // measurement build only (MPA_LSQP_DBG): 1 = no DMA, 2 = no compute
   int grp0[kMaxLsqTasks + 1];
   LsqpTask t[kMaxLsqTasks];
 };
 hipError_t launch_lsqp(const LsqpBatch& a, hipStream_t s);
+// the same batch by the one-wave-per-SIMD cut (lsqp4_kernel.hip, the default)
+hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s);
 
 // Single-pass variant (lsqf_kernel.hip): groups of P = ceil(cols / kLsqfSlice) workgroups,
 // one 512-column slice each, exchanging per-block partial residuals through `xbuf`.

@@ -88,6 +88,16 @@ __device__ __forceinline__ void dma16(const void* src, void* lds) {
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(l) : "memory", "m0");
 }
 
+// L2 prefetch of 4 B per lane into a per-wave sink nobody reads (global_load_lds_dword): a
+// lane per 128-B line of the wave's next-but-pfd slice brings the lines into the XCD's L2
+// (and the Infinity Cache) well before the DMA asks for them, so a wave keeps HBM requests
+// in flight beyond what its two 8-KiB LDS slots hold (MI355X_MICROARCH.md §Indexed rows: ~72
+// KiB in flight per CU to hide an HBM miss; the ring gives one to two slots per wave)
+__device__ __forceinline__ void pf4(const void* src, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(l) : "memory", "m0");
+}
+
 // 16-B chunk c (8 columns) of slice row r is stored at chunk position c ^ swz(r): distinct
 // bank groups for the 16 rows a ds_read_b128 lane group touches (phase 1) and for the 8
 // rows x 2 chunks a ds_read_b64_tr_b16 half-wave touches (phase 2)
@@ -118,6 +128,7 @@ __global__ void __launch_bounds__(PT, 2) lsqp_kernel(LsqpBatch batch) {
   __shared__ __attribute__((aligned(16))) uint8_t bring[2][PRB * PH * 2];
   __shared__ __attribute__((aligned(16))) f32x4 part[PW][2][64];
   __shared__ __attribute__((aligned(16))) uint8_t rimg[2 * 16 * RS];
+  __shared__ __attribute__((aligned(16))) uint32_t sink[PW][64];
 
   // blocks b and b + 8 are the two halves of one pair (one XCD under round-robin placement;
   // speed only): pair index = (b / 16) * 8 + b % 8
@@ -203,16 +214,32 @@ __global__ void __launch_bounds__(PT, 2) lsqp_kernel(LsqpBatch batch) {
     dma16(Bm + row * K + PH * h + 8 * bpiece, bslot);
   };
 
+  // the L2 prefetch of block kb: lane = (row lane / 4, 128-B line lane % 4) of the wave's slice
+  const int pfd = batch.pfd;
+  auto pf = [&](int64_t kb) __attribute__((always_inline)) {
+    const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
+    int64_t row = kc * PRB + (lane >> 2);
+    row = row < rows ? row : rows - 1;
+    const int col = c0 + 64 * (lane & 3) < cols ? c0 + 64 * (lane & 3) : 0;
+    pf4(A + row * lda + col, &sink[w][0]);
+  };
+
   f32x4 G[2][16];  // G^T tiles: [iterate tile][column tile], lane (i, g): rows (its) 4g + r, column i
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int ct = 0; ct < 16; ++ct) G[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // the prologue issues what two earlier steps would have (DMA, B, prefetch pfd blocks ahead
+  // of it), so every step's wait below counts the same loads; blocks 2 .. pfd - 1 are
+  // prefetched first (older than everything the waits count)
+  for (int d = 2; d < pfd; ++d) pf(kb0 + d);
   dma(kb0, my0);
   if (w == 0) dma_b(kb0, bring[0]);
+  if (pfd) pf(kb0 + pfd);
   dma(kb0 + 1, my1);
   if (w == 0) dma_b(kb0 + 1, bring[1]);
+  if (pfd) pf(kb0 + 1 + pfd);
 
   const int qq = (lane >> 2) & 3, p4 = lane & 3;
   // LDS offsets inside a slot (the swizzle of row r touches chunk bits 1-3 only, so k-steps
@@ -227,10 +254,16 @@ __global__ void __launch_bounds__(PT, 2) lsqp_kernel(LsqpBatch batch) {
   }
   // one block: slot / bv hold block u (static buffers: the loop below is unrolled by two)
   auto step = [&](int u, uint8_t* slot, const uint8_t* bslot) __attribute__((always_inline)) {
-    // this block's DMA has landed: all but the youngest loads (the next block's 8 pieces, and
-    // wave 0's B piece) are done.  vmcnt(8) / vmcnt(9): expcnt / lgkmcnt fields left free
-    if (w == 0) __builtin_amdgcn_s_waitcnt(0x0F79);
-    else __builtin_amdgcn_s_waitcnt(0x0F78);
+    // this block's DMA has landed: all but the youngest loads (the next block's 8 pieces,
+    // wave 0's B piece, and with prefetch on the two prefetches issued after this block's
+    // DMA) are done.  vmcnt(8 .. 11): expcnt / lgkmcnt fields left free
+    if (pfd) {
+      if (w == 0) __builtin_amdgcn_s_waitcnt(0x0F7B);
+      else __builtin_amdgcn_s_waitcnt(0x0F7A);
+    } else {
+      if (w == 0) __builtin_amdgcn_s_waitcnt(0x0F79);
+      else __builtin_amdgcn_s_waitcnt(0x0F78);
+    }
     // ---- phase 1: P_w[rows 4g + r][iterate 16 t + i] over this wave's k-steps
     f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -289,6 +322,7 @@ __global__ void __launch_bounds__(PT, 2) lsqp_kernel(LsqpBatch batch) {
     lgkm_drain();
     dma(kb0 + u + 2, slot);
     if (w == 0) dma_b(kb0 + u + 2, const_cast<uint8_t*>(bslot));
+    if (pfd) pf(kb0 + u + 2 + pfd);
   };
   for (int u = 0; u < nb; u += 2) {
     step(u, my0, bring[0]);

@@ -331,6 +331,9 @@ class HipComm final : public Comm {
     const char* cb = std::getenv("MPA_COORD_BATCH");
     coord_batches_ = !(cb && *cb == '0');
     fused_tail_ = !env_off("MPA_TAIL");
+    { const char* e = std::getenv("MPA_LSQP_SHARE"); lsqp_share_ = e && *e == '1'; }
+    { const char* e = std::getenv("MPA_LSQP"); lsqp8_ = e && *e == '8'; }
+    if (const char* e = std::getenv("MPA_LSQP_PF")) lsqp_pfd_ = std::max(0, std::min(8, std::atoi(e)));
     const char* dbg = std::getenv("MPA_DEBUG");
     debug_ = dbg && *dbg == '1';
     if (debug_ && region_) {
@@ -708,7 +711,7 @@ class HipComm final : public Comm {
       b.t[0].go = w.cancel_dev;
       enqueue_lsq(b, ts.dtype, int(ts.cols), w.stream, bytes, rank);
     } else {
-      LsqbLaunch b = build_lsqb_batch({rank}, &bytes);
+      LsqbLaunch b = build_lsqb_batch({rank}, &bytes, armed_share());
       b.set_go(w.cancel_dev);
       enqueue_lsqb(b, w.stream, bytes, rank);
     }
@@ -1503,6 +1506,7 @@ class HipComm final : public Comm {
   // the two passes (lsqb_kernel.hip).
   struct LsqbLaunch {
     bool pair = false;   // lsqp (the default single pass)
+    bool pair8 = false;  // ... by the eight-wave cut (MPA_LSQP=8)
     bool fused = false;  // lsqf (opt-in)
     bool quad = false;   // lsqq
     LsqbBatch two{};
@@ -1558,7 +1562,19 @@ class HipComm final : public Comm {
 
   // kernel arguments over `ranks`; advances the workers' counter bases.  Algorithmic bytes
   // per task: A + B + X + G.
-  LsqbLaunch build_lsqb_batch(const std::vector<int64_t>& ranks, double* bytes_out) {
+  // workers of this process with a batched least-squares task: a single-pass launch gives
+  // each of its tasks the grid share of one of them, so that the launches of one epoch (all
+  // fresh tasks, then a stale worker's re-dispatch, src/MPIAsyncPools.jl:177-184) run side
+  // by side on disjoint CUs instead of the later one queueing behind a full-chip grid
+  int lsqb_share() const {
+    if (!lsqp_share_) return 1;
+    int k = 0;
+    for (int64_t r = 1; r <= nworkers_; ++r)
+      k += w_[size_t(r - 1)].here && tasks_[size_t(r - 1)].kind == MPA_TASK_LSQ_BATCH;
+    return k > 0 ? k : 1;
+  }
+
+  LsqbLaunch build_lsqb_batch(const std::vector<int64_t>& ranks, double* bytes_out, int share = 0) {
     LsqbLaunch L;
     double bytes = 0;
     for (int64_t rank : ranks) {
@@ -1569,10 +1585,15 @@ class HipComm final : public Comm {
     *bytes_out = bytes;
     if (lsqp_enabled(ranks) && !lsqf_enabled(ranks) && !lsqq_enabled(ranks)) {
       L.pair = true;
+      L.pair8 = lsqp8_;
       LsqpBatch& b = L.halves;
       b.ntasks = int(ranks.size());
-      // one workgroup per CU: 128 pairs (256 workgroups), dealt evenly over the tasks
+      b.pfd = lsqp_pfd_ >= 0 ? lsqp_pfd_ : (lsqp8_ ? 0 : 1);
+      { const char* d = MPA_MEASURE ? std::getenv("MPA_LSQP_DBG") : nullptr; b.dbg = d ? std::atoi(d) : 0; }
+      // one workgroup per CU: 128 pairs (256 workgroups), dealt evenly over max(tasks,
+      // share) tasks
       constexpr int target = 128;
+      const int split = std::max(b.ntasks, share > 0 ? share : lsqb_share());
       int pairs = 0;
       for (int k = 0; k < b.ntasks; ++k) {
         const int64_t rank = ranks[size_t(k)];
@@ -1590,7 +1611,7 @@ class HipComm final : public Comm {
         t.rows = ts.rows;
         t.lda = ts.lda;
         t.cols = int(ts.cols);
-        const int per = target / b.ntasks + (k < target % b.ntasks ? 1 : 0);
+        const int per = target / split + (k < target % split ? 1 : 0);
         const int64_t nblocks = (ts.rows + 15) / 16;
         const int ng = int(std::max<int64_t>(1, std::min<int64_t>(std::min(per, kLsqpMaxGroups), nblocks)));
         b.grp0[k] = pairs;
@@ -1741,9 +1762,11 @@ class HipComm final : public Comm {
       HIPCHECK(hipEventRecord(tl.start, s));
     }
 #if MPA_MEASURE
-    HIPCHECK(b.pair ? launch_lsqp(b.halves, s) : b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
+    HIPCHECK(b.pair ? (b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
+                    : b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #else
-    HIPCHECK(b.pair ? launch_lsqp(b.halves, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
+    HIPCHECK(b.pair ? (b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
+                    : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #endif
     if (timed) {
       HIPCHECK(hipEventRecord(tl.stop, s));
@@ -1933,6 +1956,15 @@ class HipComm final : public Comm {
   // the epoch step of the next ahead epoch is already enqueued in a tail (tail_pending_)
   uint32_t* tail_ctr_ = nullptr;
   bool fused_tail_ = true;  // MPA_TAIL=0: a separate epoch kernel every epoch
+  // MPA_LSQP_SHARE=1: a single-pass launch's grid is dealt as if every local batched worker
+  // ran in it (off: batches share the coordinator stream, so a partial grid idles CUs; c5
+  // 19.9 vs 11.1 ms per epoch, profiles/r02_c5_lsqp_tuning.txt)
+  bool lsqp_share_ = false;
+  bool lsqp8_ = false;  // MPA_LSQP=8: the eight-wave single pass (lsqp_kernel.hip)
+  // lsqp L2 prefetch lead in blocks (MPA_LSQP_PF; 0 = off; unset: 1 for lsqp4, 0 for the
+  // eight-wave cut).  lsqp4: 1 block 8.47 ms vs 9.50 without, 2-4 slower (L2 thrash);
+  // profiles/r02_c5_lsqp_tuning.txt
+  int lsqp_pfd_ = -1;
   bool tail_next_ = false, tail_pending_ = false;
   size_t tail_ranks_ = 0;
   EpochArgs tail_args_{};

@@ -193,14 +193,15 @@ def test_lsqb_descent_native_loop_matches_python_loop(M, monkeypatch, env):
     assert float(torch.linalg.norm(outs[0][0])) > 0
 
 
-@pytest.mark.parametrize("env", [{}, {"MPA_LSQP": "0"}, {"MPA_LSQF": "1"}, {"MPA_LSQF": "1", "MPA_LSQF_DBG": "7"},
-                                 {"MPA_LSQQ": "1"}],
-                         ids=["lsqp_pairs_default", "two_pass", "lsqf_xcd_local_groups", "lsqf_cross_xcd_groups",
-                              "lsqq_quads"])
+@pytest.mark.parametrize("env", [{}, {"MPA_LSQP": "8"}, {"MPA_LSQP": "0"}, {"MPA_LSQF": "1"},
+                                 {"MPA_LSQF": "1", "MPA_LSQF_DBG": "7"}, {"MPA_LSQQ": "1"}],
+                         ids=["lsqp4_pairs_default", "lsqp_eight_waves", "two_pass", "lsqf_xcd_local_groups",
+                              "lsqf_cross_xcd_groups", "lsqq_quads"])
 @pytest.mark.parametrize("rows,cols,n", [(1, 32, 1), (4113, 544, 1), (3000, 2048, 3), (20000, 1024, 2)])
 def test_single_pass_vs_oracle(M, monkeypatch, env, rows, cols, n):
     """Every c5 kernel against the oracle: the default single pass by iterate halves
-    (lsqp_kernel.hip: pairs of workgroups, no exchange), the two passes (MPA_LSQP=0), and
+    (lsqp4_kernel.hip: pairs of workgroups of one wave per SIMD, no exchange), the same
+    scheme cut into eight waves (lsqp_kernel.hip, MPA_LSQP=8), the two passes (MPA_LSQP=0), and
     the opt-in single pass lsqf_kernel.hip (MPA_LSQF=1),
     groups of P = ceil(cols / 512) workgroups exchanging partial residuals inside an XCD
     (plain stores through the shared L2) or, with MPA_LSQF_DBG=7, every group treated as

@@ -51,14 +51,16 @@ def main():
     globals()["KERNEL"] = a.kernel
     f = per_dispatch(a.fetch, "FETCH_SIZE")[a.skip:]
     w = per_dispatch(a.write, "WRITE_SIZE")[a.skip:]
-    fetch_kib, write_kib = statistics.median(f), statistics.median(w)
+    # mean over the dispatches (the c5 bench alternates 1-task and 7-task launches; its
+    # alg_bytes_per_launch is a mean too)
+    fetch_kib, write_kib = statistics.fmean(f), statistics.fmean(w)
     read_b = 2.0 * fetch_kib * 1024.0  # gfx950: FETCH_SIZE = half of wide streaming reads
     write_b = write_kib * 1024.0
     out = {
         "kernel": KERNEL,
         "dispatches": {"fetch": len(f), "write": len(w)},
-        "fetch_size_kib_median": fetch_kib,
-        "write_size_kib_median": write_kib,
+        "fetch_size_kib_mean": fetch_kib,
+        "write_size_kib_mean": write_kib,
         "hbm_read_bytes_per_launch": read_b,
         "hbm_write_bytes_per_launch": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
