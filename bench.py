@@ -168,8 +168,11 @@ def delay_schedule(cfg, seed, w, count=4096):
 
 def kernel_name(cfg):
     if cfg.get("iterates", 1) > 1:
-        if os.environ.get("MPA_LSQP", "1") != "0" and cfg["cols"] <= 2048:
-            return "lsqp_kernel (bf16 MFMA single pass by iterate halves, one launch per batch)"
+        v = os.environ.get("MPA_LSQP", "1")
+        if v == "8" and cfg["cols"] <= 2048:
+            return "lsqp_kernel (bf16 MFMA single pass by iterate halves, eight waves, one launch per batch)"
+        if v != "0" and cfg["cols"] <= 2048:
+            return "lsqp4_kernel (bf16 MFMA single pass by iterate halves, one wave per SIMD, one launch per batch)"
         return "lsqb_resid_kernel + lsqb_grad_kernel (bf16 MFMA, two launches per batch)"
     return "lsq_grad_kernel (one batched launch per epoch per GPU)"
 
@@ -224,7 +227,10 @@ def report(args, cfg, world, el, per_rank, extra):
     if os.path.exists(pmc) and world == 1:
         try:
             d = json.load(open(pmc))
-            traffic = d.get("hbm_bytes_per_launch")
+            # per launch of THIS run: the measured traffic / algorithmic-bytes ratio times this
+            # run's mean algorithmic bytes per launch (launches of the c5 bench carry 1, 7 or 8
+            # tasks, so the summary is per task there)
+            traffic = round(d["traffic_over_alg"] * per_launch_bytes, 1) if d.get("traffic_over_alg") else None
             traffic_src = "%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py, %s; not this run)" % (
                 os.path.relpath(pmc, ROOT), d.get("date", "round-1 box"))
         except Exception:
@@ -278,13 +284,20 @@ def report(args, cfg, world, el, per_rank, extra):
 
 
 ROCPROF_STATS = {"c2": ("r02_c2_kernel_stats.csv", "lsq_grad_kernel"),
-                 "c5": ("r02_c5_kernel_stats.csv", "lsqp_kernel")}
+                 "c5": ("r02_c5_kernel_stats.csv", "lsqp4_kernel")}
 
 
 def rocprof_avg_ms(cfg):
-    """(average ms, source) of the dominant kernel in the committed rocprofv3 --stats summary
-    of this config's bench command (profiles/), or None."""
+    """(average ms, source) of the dominant kernel under rocprofv3 in the committed profiles
+    of this config's bench command: the timed-region window of its kernel trace
+    (tools/trace_window.py) where committed, else the --stats summary; None without either."""
     name, kernel = ROCPROF_STATS.get(cfg["config"], (None, None))
+    win = os.path.join(ROOT, "profiles", "r02_%s_rocprof_window.json" % cfg["config"])
+    if name and os.path.exists(win):
+        d = json.load(open(win))
+        if d.get("kernel") == kernel:
+            return round(d["avg_ms"], 4), "profiles/%s (last %d launches of the traced run = its timed region; %s)" % (
+                os.path.basename(win), d["launches"], d.get("date", ""))
     path = os.path.join(ROOT, "profiles", name) if name else None
     if not path or not os.path.exists(path):
         return None

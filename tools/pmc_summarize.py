@@ -44,27 +44,37 @@ def main():
     p.add_argument("--fetch", required=True)
     p.add_argument("--write", required=True)
     p.add_argument("--out", required=True)
-    p.add_argument("--alg-bytes", type=float, required=True, help="algorithmic bytes per launch")
+    p.add_argument("--alg-bytes", type=float, required=True,
+                   help="algorithmic bytes per launch (per task with --task-bytes)")
+    p.add_argument("--task-bytes", type=float, default=0.0,
+                   help="launches carry a varying number of equal tasks (the c5 bench: 8-, 7- and "
+                        "1-task launches): tasks per dispatch = round(HBM bytes / this), and the "
+                        "summary is per task")
     p.add_argument("--skip", type=int, default=2, help="leading dispatches to drop (warm-up)")
     p.add_argument("--kernel", default=KERNEL, help="kernel name substring")
     a = p.parse_args()
     globals()["KERNEL"] = a.kernel
     f = per_dispatch(a.fetch, "FETCH_SIZE")[a.skip:]
     w = per_dispatch(a.write, "WRITE_SIZE")[a.skip:]
-    # mean over the dispatches (the c5 bench alternates 1-task and 7-task launches; its
-    # alg_bytes_per_launch is a mean too)
-    fetch_kib, write_kib = statistics.fmean(f), statistics.fmean(w)
-    read_b = 2.0 * fetch_kib * 1024.0  # gfx950: FETCH_SIZE = half of wide streaming reads
-    write_b = write_kib * 1024.0
+    # gfx950: FETCH_SIZE = half of the bytes of wide streaming reads; both counters in KiB
+    rd = [2.0 * v * 1024.0 for v in f]
+    wr = [v * 1024.0 for v in w]
+    unit = "launch"
+    if a.task_bytes > 0:
+        tr = [max(1, round(v / a.task_bytes)) for v in rd]
+        tw = [max(1, round(v * (sum(rd) / sum(wr)) / a.task_bytes)) for v in wr]
+        read_b, write_b = sum(rd) / sum(tr), sum(wr) / sum(tw)
+        unit = "task"
+    else:
+        read_b, write_b = statistics.fmean(rd), statistics.fmean(wr)
     out = {
         "kernel": KERNEL,
         "dispatches": {"fetch": len(f), "write": len(w)},
-        "fetch_size_kib_mean": fetch_kib,
-        "write_size_kib_mean": write_kib,
-        "hbm_read_bytes_per_launch": read_b,
-        "hbm_write_bytes_per_launch": write_b,
-        "hbm_bytes_per_launch": read_b + write_b,
-        "alg_bytes_per_launch": a.alg_bytes,
+        "unit": unit,
+        "hbm_read_bytes_per_" + unit: read_b,
+        "hbm_write_bytes_per_" + unit: write_b,
+        "hbm_bytes_per_" + unit: read_b + write_b,
+        "alg_bytes_per_" + unit: a.alg_bytes,
         "traffic_over_alg": (read_b + write_b) / a.alg_bytes,
         "date": time.strftime("%Y-%m-%d"),
         "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes",

@@ -1,0 +1,45 @@
+"""Average duration of a kernel over the timed region of a bench run traced by
+`rocprofv3 --kernel-trace --stats`: the last N launches of the kernel in the trace, N = the
+`roofline.launches` of the bench line that run printed (the warm-up launches before the
+timed region are dropped; the c5 bench mixes 8-, 7- and 1-task launches, so an all-launch
+average of the --stats summary is not comparable with the timed-region figure).
+
+    python tools/trace_window.py --trace DIR/c5_kernel_trace.csv --bench-log DIR/../c5_trace.log \
+        --kernel lsqp4_kernel --out profiles/r02_c5_rocprof_window.json
+"""
+import argparse
+import csv
+import json
+import time
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--trace", required=True)
+    p.add_argument("--bench-log", required=True, help="stdout of the traced bench run (its JSON line)")
+    p.add_argument("--kernel", required=True)
+    p.add_argument("--out", required=True)
+    a = p.parse_args()
+    line = [ln for ln in open(a.bench_log) if ln.startswith("{")][-1]
+    bench = json.loads(line)
+    n = int(bench["roofline"]["launches"])
+    rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows][-n:]
+    out = {
+        "kernel": a.kernel,
+        "launches": len(ms),
+        "avg_ms": sum(ms) / len(ms),
+        "sum_ms": sum(ms),
+        "bench_avg_launch_ms_same_run": bench["roofline"]["avg_launch_ms"],
+        "bench_steps": bench["steps"],
+        "source": "rocprofv3 --kernel-trace of bench.py (the last `launches` dispatches = the timed region)",
+        "date": time.strftime("%Y-%m-%d"),
+    }
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
