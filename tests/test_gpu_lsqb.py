@@ -3,17 +3,18 @@ G_i = A_i^T (A_i X - B_i), bf16 A/B/X, fp32 accumulate (lsqb_kernel.hip), throug
 C ABI (mpa_comm_set_task_lsq_batch + mpa_asyncmap), against the fp64 oracle
 (oracle/lsq.py batched_shard_gradient) on the same bf16-rounded inputs.
 
-Tolerance: normwise relative 1e-4.  The kernel carries the residual between its two
-passes as bf16 hi + lo (~2^-17 relative per element) and accumulates in fp32 over up to
-2^20 rows; BASELINE states 1e-5 for fp32 *inputs*, and for bf16 inputs/fp32 accumulate
-this 1e-4 is the stated bound (the measured error is printed, typically ~1e-6).
+Tolerance: normwise relative 1e-5, set from evidence.  Every kernel carries the residual
+as bf16 hi + lo (~2^-17 relative per element) and accumulates in fp32 over up to 2^20 rows;
+over every case of this file and every kernel the worst measured error is 2.42e-6
+(profiles/r02_c5_tolerance.txt: the default lsqp4, the eight-wave lsqp, the two passes,
+lsqf), so 1e-5 is about 4x the worst case and equals BASELINE's fp32 tolerance.
 """
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 K = 64
-TOL = 1e-4
+TOL = 1e-5
 
 
 @pytest.fixture(scope="module")
