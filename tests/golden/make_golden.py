@@ -185,13 +185,15 @@ def scenarios():
         separate(s, 4 * MS)
         s["min_gap_ns"] = min_completion_gap(s)
         sc.append(s)
-    # BASELINE configs[3] (c4: worker 1 + 5 of the other 7, stale results folded in) and
+    # BASELINE configs[3] (c4: worker 1 + 5 of the other 7, stale results folded in),
     # configs[0] (c1: 3 workers, nwait 2, the 10 epochs of examples/iterative_example.jl:37)
+    # and configs[2] (c3: 6 of 8)
     # replayed on device with least-squares workers (tests/test_gpu_configs.py); own seed so
     # the scenarios above stay unchanged
     rng2 = np.random.default_rng(20261016)
     for name, n, nw, k, drain in (("gpu_sep_c4_first_plus_5", 8, "first_plus_5", 12, True),
-                                  ("gpu_sep_c1", 3, 2, 10, False)):
+                                  ("gpu_sep_c1", 3, 2, 10, False),
+                                  ("gpu_sep_c3", 8, 6, 12, False)):
         d = rng2.integers(5, 41, size=(n, 64)) * MS
         s = {"name": name, "n": n, "worker": "kmap2", "durations_ns": d.ravel().tolist(),
              "ops": [{"op": "asyncmap", "nwait": nw, "send": e} for e in range(1, k + 1)] +
