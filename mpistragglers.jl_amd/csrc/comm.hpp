@@ -55,6 +55,14 @@ class Comm {
   virtual int64_t waitany(int64_t n, const int64_t* ranks, const uint8_t* live) = 0;
   virtual void waitall(int64_t n, const int64_t* ranks, const uint8_t* live) = 0;
   virtual void flush() = 0;
+  // the flush of a stale worker's re-dispatch inside the wait loop (src/MPIAsyncPools.jl:
+  // 177-184); a transport may hold the task's launch back until its next flush or until a
+  // wait would block (HIP: the task then joins the next epoch's batched launch)
+  virtual void flush_stale() { flush(); }
+  // before each waitany of the wait loop: true when the results still owed by tasks posted
+  // in phase 2 of this call already satisfy an integer nwait, so a held re-dispatch need not
+  // be launched for the call to finish (false: a wait that would block launches it first)
+  virtual void set_wait_hold(bool may_hold) { (void)may_hold; }
   virtual void end_call() = 0;
   virtual uint64_t now_ns() = 0;
 

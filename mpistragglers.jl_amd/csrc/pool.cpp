@@ -90,11 +90,17 @@ void asyncmap(Pool& p, const AsyncmapArgs& a) {
     p.active[k] = 0;                                                               // :110
   }                                                                                // :113 Wait!(sreq): no-op
 
+  // owed[i]: worker i was sent this epoch's message in phase 2 and has not replied (a
+  // transport hint only: set_wait_hold below; the state machine does not read it)
+  std::vector<uint8_t> owed(size_t(comm_size), 0);
+  int64_t nowed = 0;
   for (int64_t i = 0; i < comm_size; ++i) {                                        // :118-139
     const size_t k = size_t(i);
     if (p.active[k]) continue;                                                     // :121-123
     p.active[k] = 1;                                                               // :126
     dispatch(p, c, i, a.tag);                                                      // :130-138
+    owed[k] = 1;
+    ++nowed;
   }
   c.flush();  // phase-1 copies, then the sends of phase 2, in the reference's order
 
@@ -111,6 +117,7 @@ void asyncmap(Pool& p, const AsyncmapArgs& a) {
       fail(MPA_ERROR, "nwait must be either an Integer or a Function, but is a %s",
            a.nwait_typename ? a.nwait_typename : "?");
     }
+    c.set_wait_hold(a.nwait_kind == MPA_NWAIT_INT && nowed >= a.nwait - nrecv);
     const int64_t i = c.waitany(comm_size, p.ranks.data(), p.rreq_live.data());   // :161
     if (i < 0) {  // MPI_UNDEFINED: undefined in the reference; an error here
       c.end_call();
@@ -118,13 +125,17 @@ void asyncmap(Pool& p, const AsyncmapArgs& a) {
     }
     const size_t k = size_t(i);
     p.rreq_live[k] = 0;
+    if (owed[k]) {
+      owed[k] = 0;
+      --nowed;
+    }
     harvest(p, c, i);                                                              // :164-168
     if (p.repochs[k] == p.epoch) {                                                 // :174-176
       nrecv += 1;
       p.active[k] = 0;
     } else {                                                                       // :177-184
       dispatch(p, c, i, a.tag);
-      c.flush();  // the stale chunk must reach recvbuf before the worker overwrites it
+      c.flush_stale();  // the stale chunk must reach recvbuf before the worker overwrites it
     }
   }
   c.end_call();

@@ -333,6 +333,7 @@ class HipComm final : public Comm {
     fused_tail_ = !env_off("MPA_TAIL");
     { const char* e = std::getenv("MPA_LSQP_SHARE"); lsqp_share_ = e && *e == '1'; }
     { const char* e = std::getenv("MPA_LSQP"); lsqp8_ = e && *e == '8'; }
+    hold_ok_ = !env_off("MPA_HOLD");
     if (const char* e = std::getenv("MPA_LSQP_PF")) lsqp_pfd_ = std::max(0, std::min(8, std::atoi(e)));
     const char* dbg = std::getenv("MPA_DEBUG");
     debug_ = dbg && *dbg == '1';
@@ -346,6 +347,7 @@ class HipComm final : public Comm {
 
   ~HipComm() override {
     try {
+      release_held();
       disarm_all();
     } catch (...) {
     }
@@ -445,6 +447,11 @@ class HipComm final : public Comm {
     bool any = false;
     for (int64_t i = 0; i < n; ++i) any |= live[i] != 0;
     if (!any) return -1;
+    if (!held_.empty() && !may_hold_) {  // the wait would block: held launches go first
+      for (int64_t i = 0; i < n; ++i)
+        if (live[i] && done(ranks[i])) return i;
+      release_held();
+    }
     const auto t0 = Clock::now();
     for (uint64_t spins = 0;; ++spins) {
       for (int64_t i = 0; i < n; ++i)
@@ -455,6 +462,7 @@ class HipComm final : public Comm {
   }
 
   void waitall(int64_t n, const int64_t* ranks, const uint8_t* live) override {
+    release_held();
     const auto t0 = Clock::now();
     for (int64_t i = 0; i < n; ++i) {
       if (!live[i]) continue;
@@ -504,7 +512,29 @@ class HipComm final : public Comm {
   }
 
   void end_call() override {
+    may_hold_ = false;
     if (!defer_end_) flush();
+  }
+
+  // A stale worker's re-dispatch (pool.cpp, the wait loop): its message copies and the
+  // stale harvest go out now, its task launch is HELD (undelayed least-squares tasks only)
+  // and joins the next flush's batch, or is launched when a wait would block.  On one GPU
+  // the coordinator stream runs launches in order, so a re-dispatch enqueued behind the
+  // running batch starts when that batch ends either way; held, it runs INSIDE the next
+  // epoch's batched launch instead of alone before it (c5, nwait 7 of 8: one 8-task launch
+  // per epoch instead of a 1-task launch and a 7-task launch, profiles/r02_c5_hold_ab.txt).
+  // The pool's state machine is unchanged; MPA_HOLD=0 launches re-dispatches at once.
+  void flush_stale() override {
+    hold_next_ = hold_ok_;
+    flush();
+    hold_next_ = false;
+  }
+  void set_wait_hold(bool may_hold) override { may_hold_ = may_hold; }
+  void release_held() {
+    if (held_.empty()) return;
+    std::vector<int64_t> h;
+    h.swap(held_);
+    launch_tasks(h, /*staged=*/false);
   }
 
   // ---- the native descent loop (capi.cpp descent_loop) ----
@@ -560,6 +590,7 @@ class HipComm final : public Comm {
   }
 
   void shutdown() override {
+    release_held();
     if (role_ != SERVER) {
       const auto t0 = Clock::now();
       for (int64_t r = 1; r <= nworkers_; ++r) {
@@ -772,8 +803,18 @@ class HipComm final : public Comm {
   // tasks of the workers served here among `posted`, behind the exchange / epoch kernel
   void launch_local(const std::vector<int64_t>& posted) {
     std::vector<int64_t> here;
-    for (int64_t rank : posted)
-      if (!w_[size_t(rank - 1)].remote) here.push_back(rank);
+    for (int64_t rank : posted) {
+      if (w_[size_t(rank - 1)].remote) continue;
+      const TaskSpec& ts = tasks_[size_t(rank - 1)];
+      if (hold_next_ && (ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty())
+        held_.push_back(rank);  // flush_stale(): joins the next batch
+      else
+        here.push_back(rank);
+    }
+    if (!here.empty() && !held_.empty() && !hold_next_) {  // held re-dispatches join this batch
+      here.insert(here.begin(), held_.begin(), held_.end());
+      held_.clear();
+    }
     // every task of this call is awaited before the caller enqueues anything else on the
     // coordinator stream: run the batch right behind the exchange on that stream (a
     // cross-queue event wait costs ~35 us per epoch, profiles/r01_c2_gaps.json)
@@ -901,7 +942,7 @@ class HipComm final : public Comm {
     auto skip = [this]() {
       if (tail_pending_) fail(MPA_ERROR, "fused tail: the epoch it prepared was not enqueued ahead");
     };
-    if (ahead_left_ <= 0 || !b_.await_all || int64_t(call_posts_.size()) != b_.n) return skip();
+    if (ahead_left_ <= 0 || !b_.await_all || int64_t(call_posts_.size()) != b_.n || !held_.empty()) return skip();
     UpdateSpec& u = ahead_pred_;
     for (const auto& cp : call_posts_)
       if (w_[size_t(cp.rank - 1)].preposted) return skip();
@@ -1960,6 +2001,10 @@ class HipComm final : public Comm {
   // ran in it (off: batches share the coordinator stream, so a partial grid idles CUs; c5
   // 19.9 vs 11.1 ms per epoch, profiles/r02_c5_lsqp_tuning.txt)
   bool lsqp_share_ = false;
+  bool hold_ok_ = true;     // MPA_HOLD=0: a stale re-dispatch launches at once (flush_stale)
+  bool hold_next_ = false;  // set while flush_stale() flushes
+  bool may_hold_ = false;   // this call's wait completes without the held tasks (set_wait_hold)
+  std::vector<int64_t> held_;  // held re-dispatches, launched with the next batch
   bool lsqp8_ = false;  // MPA_LSQP=8: the eight-wave single pass (lsqp_kernel.hip)
   // lsqp L2 prefetch lead in blocks (MPA_LSQP_PF; 0 = off; unset: 1 for lsqp4, 0 for the
   // eight-wave cut).  lsqp4: 1 block 8.47 ms vs 9.50 without, 2-4 slower (L2 thrash);
