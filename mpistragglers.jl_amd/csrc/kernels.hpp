@@ -84,7 +84,17 @@ struct LsqTask {
   // to seq means "disarmed", and the task returns without computing or publishing (NULL:
   // not armed)
   const unsigned long long* go;
+  // wide rows (cols > 2048, lsqw_kernel.hip): the residual r = A x - b (rows T), the
+  // per-slice tree and slice-completion counters, and the row groups of the second pass
+  void* r;
+  uint32_t* wctr;
+  int grid2;
 };
+// Wide rows: two passes (r = A x - b, then g = A^T r over 2048-column slices), A read twice.
+constexpr int kLsqWideSlice = 2048;   // columns per slice (fp32: 8 x 16 B per lane, fp64: 16)
+constexpr int kLsqWideMaxCols = 65536;
+constexpr int kLsqWideMaxGroups = 64;  // row groups per slice in the second pass (fan-in-8 tree)
+constexpr int kLsqWideCtrPerSlice = 16;
 constexpr unsigned long long kCancelBit = 1ull << 62;
 
 // Reduction tree of a least-squares task (lsq_kernel.hip): fan-in, most workgroups per
@@ -111,8 +121,10 @@ struct LsqBatch {
   uint32_t* tail_ctr;  // task completions of this launch (the last one resets it)
   EpochArgs ep;
 };
-// Returns hipErrorInvalidValue if no kernel variant covers (dtype, cols).
+// Returns hipErrorInvalidValue if no kernel variant covers (dtype, cols).  cols > 2048 runs
+// the wide two passes (launch_lsqw).
 hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s);
+hipError_t launch_lsqw(int dtype, const LsqBatch& a, hipStream_t s);
 const char* lsq_variant_name();  // the c2-shape kernel variant in use (MPA_LSQ_VARIANT)
 int lsq_set_variant(int i);      // returns the number of variants, or -1 if i is out of range
 // Shape helpers for the launcher's variant table.

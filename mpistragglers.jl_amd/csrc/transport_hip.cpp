@@ -66,6 +66,7 @@ using Clock = std::chrono::steady_clock;
 // same-box bench A/B in profiles/r01_lsq_grid_ab.txt: c2 +6-7 %, c3/c4 unchanged); the read
 // probe (mpa_read_bandwidth) shows the same shape: fewer, longer streams read faster
 constexpr int kDefaultLaunchGrid = 192;
+constexpr int kWideResidGrid = 1024;  // wide rows: pass-1 workgroups per launch (a wave per row)
 constexpr int kSlabGridCap = kLsqMaxGrid;  // most workgroups a single task may be given
 constexpr int kLaunchStreams = 2;
 // batched multi-iterate task: pass-1 / pass-2 workgroups per launch (= resident: 1 x 512 /
@@ -140,6 +141,8 @@ struct HipWorker {
   unsigned long long seq = 0;  // coordinator: tasks posted; server: tasks served
   void* slab = nullptr;
   int slab_grid = 0;
+  size_t slab_bytes = 0;
+  uint32_t* wctr = nullptr;  // wide rows (lsqw_kernel.hip): per-slice tree + completion counters
   // batched multi-iterate task (lsqb_kernel.hip): residual scratch, pass-2 partials,
   // counters and their running totals
   void* lsqb_R = nullptr;
@@ -356,6 +359,7 @@ class HipComm final : public Comm {
     if (const char* d = MPA_MEASURE ? std::getenv("MPA_LSQF_DBG") : nullptr; d && (std::atoi(d) & 16)) lsqf_prof_dump();
     for (auto& w : w_) {
       if (w.slab) (void)hipFree(w.slab);
+      if (w.wctr) (void)hipFree(w.wctr);
       if (w.lsqb_R) (void)hipFree(w.lsqb_R);
       if (w.lsqb_slab) (void)hipFree(w.lsqb_slab);
       if (w.lsqb_ctr) (void)hipFree(w.lsqb_ctr);
@@ -862,6 +866,7 @@ class HipComm final : public Comm {
       const TaskSpec& ts = tasks_[size_t(rank - 1)];
       if (w.remote || ts.kind != MPA_TASK_LSQ || !ts.delays_ns.empty() || ts.dtype != u.dtype) return false;
       const int c = lsq_cols_pad(ts.dtype, int(ts.cols));
+      if (c > kLsqWideSlice) return false;  // wide rows: two launches, no fused tail
       if (cp >= 0 && c != cp) return false;
       cp = c;
     }
@@ -1166,10 +1171,26 @@ class HipComm final : public Comm {
     if (role_ == SERVER && size_t(ts.cols) * size_t(es) > region_->max_msg())
       fail(MPA_DIMENSION_MISMATCH, "least-squares worker: %zu-byte messages exceed the mailbox", size_t(ts.cols) * es);
     const int cap = kSlabGridCap;
-    const size_t bytes = size_t(cap) * size_t(cp) * size_t(es);
-    if (!w.slab) {
+    // narrow: [grid][cols_pad] partials; wide: [slice][kLsqWideMaxGroups][2048] partials,
+    // then the residual r (rows)
+    const bool wide = cp > kLsqWideSlice;
+    const size_t bytes = wide ? size_t(cp) * kLsqWideMaxGroups * size_t(es) + size_t(ts.rows + 64) * size_t(es)
+                              : size_t(cap) * size_t(cp) * size_t(es);
+    if (bytes > w.slab_bytes) {
+      if (w.slab) {
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipFree(w.slab));
+      }
+      w.slab = nullptr;
       HIPCHECK(hipMalloc(&w.slab, bytes));
+      w.slab_bytes = bytes;
       w.slab_grid = cap;
+    }
+    if (wide && !w.wctr) {
+      const size_t n = size_t(kLsqWideMaxCols / kLsqWideSlice + 1) * kLsqWideCtrPerSlice;
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.wctr), n * sizeof(uint32_t)));
+      HIPCHECK(hipMemset(w.wctr, 0, n * sizeof(uint32_t)));
+      HIPCHECK(hipDeviceSynchronize());
     }
   }
 
@@ -1526,6 +1547,16 @@ class HipComm final : public Comm {
       t.lda = ts.lda;
       t.cols = int(ts.cols);
       t.grid = lsq_grid(ts, w, split);
+      if (ts.cols > kLsqWideSlice) {  // wide rows: pass-1 workgroups, pass-2 row groups
+        const int nslice = int((ts.cols + kLsqWideSlice - 1) / kLsqWideSlice);
+        const int es = dtype == MPA_F64 ? 8 : 4;
+        t.grid = int(std::max<int64_t>(1, std::min<int64_t>(kWideResidGrid / split, (ts.rows + 3) / 4)));
+        t.grid2 = int(std::max<int64_t>(
+            1, std::min<int64_t>({int64_t(kDefaultLaunchGrid) / split / nslice, int64_t(kLsqWideMaxGroups),
+                                  (ts.rows + 7) / 8})));
+        t.wctr = w.wctr;
+        t.r = static_cast<uint8_t*>(w.slab) + size_t(nslice) * kLsqWideSlice * kLsqWideMaxGroups * size_t(es);
+      }
       b.block0[k] = blocks;
       blocks += t.grid;
       const double es = dtype == MPA_F64 ? 8.0 : 4.0;
