@@ -191,7 +191,7 @@ struct LsqpTask {
 struct LsqpBatch {
   int ntasks;
   int pfd;  // L2 prefetch lead over the LDS-DMA, in blocks (0: none); MPA_LSQP_PF
-  int dbg;  // measurement build only (MPA_LSQP_DBG): 1 = no DMA, 2 = no compute
+  int dbg;  // measurement build only (MPA_LSQP_DBG): 1 no DMA, 2 no compute, 8/16/32 no phase 1 / reduce / phase 2
   int grp0[kMaxLsqTasks + 1];
   LsqpTask t[kMaxLsqTasks];
 };

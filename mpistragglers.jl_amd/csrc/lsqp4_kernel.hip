@@ -204,6 +204,9 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     voff[s8] = uint32_t(c0 + 8 * c < cols ? c0 + 8 * c : 0) * 2u;
   }
   const bool no_dma = MPA_MEASURE && (batch.dbg & 1), no_compute = MPA_MEASURE && (batch.dbg & 2);
+  // phase probes (measurement build): 8 no phase 1, 16 no partials / reduce / barriers, 32 no phase 2
+  const bool no_p1 = MPA_MEASURE && (batch.dbg & 8), no_red = MPA_MEASURE && (batch.dbg & 16),
+             no_p2 = MPA_MEASURE && (batch.dbg & 32);
   auto dma = [&](int64_t kb, uint8_t* slot) __attribute__((always_inline)) {
     if (no_dma) return;
     const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
@@ -293,13 +296,14 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     // ---- phase 1: P_w[rows 4g + r][iterate 16 t + i].  Fragment reads run eight k-steps
     // ahead of the MFMAs (the compiler waits for each with a counted lgkmcnt)
     constexpr int AD = 8;
+    f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if (!no_p1) {
     bf16x8 af[AD];
     auto rd1 = [&](int s) __attribute__((always_inline)) {
       return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + off1[s & 3] + 256 * (s >> 2)));
     };
 #pragma unroll
     for (int s = 0; s < AD; ++s) af[s] = rd1(s);
-    f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       __builtin_amdgcn_sched_barrier(0);
@@ -308,6 +312,8 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       if (s + AD < NKS) af[s % AD] = rd1(s + AD);
     }
     __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!no_red) {
     part[w][0][lane] = p1[0];
     part[w][1][lane] = p1[1];
     barrier();
@@ -336,6 +342,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       *reinterpret_cast<uint32_t*>(e + 32) = lw;
     }
     barrier();
+    }
     // ---- phase 2: G_w^T[it][col] += sum_k R-image[it][k] A[row(k)][col]
     bf16x8 RF[2];
 #pragma unroll
@@ -354,6 +361,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
         d[k][1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(src + 4 * ROWB));
       }
     };
+    if (!no_p2) {
     rd(0, tb[0]);
 #pragma unroll
     for (int c = 0; c < NCT / CH; ++c) {
@@ -367,6 +375,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
         G[1][CH * c + k] = mfma(RF[1], bt, G[1][CH * c + k]);
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
     }
     // the slot is read: DMA block u + 2 into it
     lgkm_drain();
