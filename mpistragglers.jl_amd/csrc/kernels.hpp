@@ -187,17 +187,32 @@ struct LsqpTask {
   int64_t rows, lda;
   int cols;
   const unsigned long long* go;  // as LsqTask::go
+  // column pairs (lsqc_kernel.hip) only
+  unsigned long long* xg;  // [kLsqpMaxGroups][2][kLsqcXR][4][64][4] {tag, fp32} exchange granules
+  int parts;               // members per row group: 2 if cols > kLsqcMemberCols, else 1
 };
 struct LsqpBatch {
   int ntasks;
-  int pfd;  // L2 prefetch lead over the LDS-DMA, in blocks (0: none); MPA_LSQP_PF
+  int pfd;  // L2 prefetch lead over the LDS-DMA, in blocks (0: none); MPA_LSQP_PF.  lsqc: phase-1 lookahead (1, 2)
   int dbg;  // measurement build only (MPA_LSQP_DBG): 1 no DMA, 2 no compute, 8/16/32 no phase 1 / reduce / phase 2
-  int grp0[kMaxLsqTasks + 1];
+  int grp0[kMaxLsqTasks + 1];  // lsqp/lsqp4: pairs before task t; lsqc: workgroups before task t
   LsqpTask t[kMaxLsqTasks];
+  // column pairs (lsqc_kernel.hip) only
+  uint32_t* tick;  // workgroup ticket counter (zero between launches: the last taker resets it)
+  unsigned* err;
+  unsigned long long spin_ticks;
 };
 hipError_t launch_lsqp(const LsqpBatch& a, hipStream_t s);
 // the same batch by the one-wave-per-SIMD cut (lsqp4_kernel.hip, the default)
 hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s);
+// Single pass by COLUMN pairs (lsqc_kernel.hip): the two members of a row group split the
+// columns (member h: columns 1024 h .. 1024 h + 1023), each holding all 64 iterates of its G
+// columns, and exchange their 16 x 64 partial products per 16-row block as tagged granules.
+// Pairs form from a ticket taken at start (members only wait for running workgroups).
+constexpr int kLsqcMemberCols = 1024;
+constexpr int kLsqcXR = 8;           // exchange ring slots per member
+constexpr int kLsqcMaxBlocks = 65535;  // 16-row blocks per row group (16-bit block field of the tag)
+hipError_t launch_lsqc(const LsqpBatch& a, hipStream_t s);
 
 // Single-pass variant (lsqf_kernel.hip): groups of P = ceil(cols / kLsqfSlice) workgroups,
 // one 512-column slice each, exchanging per-block partial residuals through `xbuf`.

@@ -159,7 +159,8 @@ struct HipWorker {
   uint32_t* lsqq_ctr = nullptr;  // quad kernel: [4] member arrivals, [4] completions (self-resetting)
   // pair single pass (lsqp_kernel.hip): G partials and tree counters (self-resetting)
   void* lsqp_slab = nullptr;
-  uint32_t* lsqp_ctr = nullptr;
+  uint32_t* lsqp_ctr = nullptr;  // [2][8][kLsqpCtrPerSlice] tree, [1] completions, then the lsqc ticket
+  unsigned long long* lsqc_xg = nullptr;  // column pairs: exchange granules
   uint32_t lsqf_sbase = 0, lsqf_tbase = 0;
   // current task
   int64_t slot = -1;
@@ -335,7 +336,13 @@ class HipComm final : public Comm {
     coord_batches_ = !(cb && *cb == '0');
     fused_tail_ = !env_off("MPA_TAIL");
     { const char* e = std::getenv("MPA_LSQP_SHARE"); lsqp_share_ = e && *e == '1'; }
-    { const char* e = std::getenv("MPA_LSQP"); lsqp8_ = e && *e == '8'; }
+    {
+      const char* e = std::getenv("MPA_LSQP");
+      lsqp8_ = e && *e == '8';
+      lsqc_ = e && *e == 'c';
+      const char* la = std::getenv("MPA_LSQC_LA");
+      lsqc_la_ = la && *la == '2' ? 2 : 1;
+    }
     hold_ok_ = !env_off("MPA_HOLD");
     if (const char* e = std::getenv("MPA_LSQP_PF")) lsqp_pfd_ = std::max(0, std::min(8, std::atoi(e)));
     const char* dbg = std::getenv("MPA_DEBUG");
@@ -369,6 +376,7 @@ class HipComm final : public Comm {
       if (w.lsqq_ctr) (void)hipFree(w.lsqq_ctr);
       if (w.lsqp_slab) (void)hipFree(w.lsqp_slab);
       if (w.lsqp_ctr) (void)hipFree(w.lsqp_ctr);
+      if (w.lsqc_xg) (void)hipFree(w.lsqc_xg);
       if (w.peer_msg) (void)hipIpcCloseMemHandle(w.peer_msg);
       if (w.peer_reply) (void)hipIpcCloseMemHandle(w.peer_reply);
       if (w.xslot) (void)hipFree(w.xslot);
@@ -1235,9 +1243,12 @@ class HipComm final : public Comm {
     }
     if (ts.cols <= kLsqpMaxCols && !w.lsqp_slab) {
       HIPCHECK(hipMalloc(&w.lsqp_slab, size_t(2) * kLsqpMaxGroups * 8 * 32 * 1024));
-      const size_t nctr = size_t(2) * 8 * kLsqpCtrPerSlice + 1;
+      const size_t nctr = size_t(2) * 8 * kLsqpCtrPerSlice + 8;  // + completions, lsqc ticket at +4
       HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqp_ctr), sizeof(uint32_t) * nctr));
       HIPCHECK(hipMemset(w.lsqp_ctr, 0, sizeof(uint32_t) * nctr));
+      const size_t xg = size_t(kLsqpMaxGroups) * 2 * kLsqcXR * 4 * 64 * 4 * sizeof(unsigned long long);
+      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqc_xg), xg));
+      HIPCHECK(hipMemset(w.lsqc_xg, 0, xg));
       HIPCHECK(hipDeviceSynchronize());
     }
     if (ts.cols <= 2048 && !w.lsqq_ctr) {
@@ -1579,6 +1590,7 @@ class HipComm final : public Comm {
   struct LsqbLaunch {
     bool pair = false;   // lsqp (the default single pass)
     bool pair8 = false;  // ... by the eight-wave cut (MPA_LSQP=8)
+    bool cpair = false;  // ... by column pairs (lsqc_kernel.hip)
     bool fused = false;  // lsqf (opt-in)
     bool quad = false;   // lsqq
     LsqbBatch two{};
@@ -1602,6 +1614,49 @@ class HipComm final : public Comm {
       if (!w_[size_t(rank - 1)].lsqp_slab || ts.cols > kLsqpMaxCols) return false;
     }
     return !ranks.empty();
+  }
+
+  // column pairs (lsqc_kernel.hip): a row group of a task with more than 1024 columns is a
+  // pair of workgroups (one each, 1024 columns and all 64 iterates), of a narrower task one
+  // workgroup; 256 workgroups (one per CU) dealt over the tasks.  Row groups of at most
+  // kLsqcMaxBlocks blocks (the tag's block field), else the iterate-halves kernel stays.
+  static int lsqc_parts(int64_t cols) { return cols > kLsqcMemberCols ? 2 : 1; }
+  int lsqc_groups(const TaskSpec& ts, int split, int k) const {
+    constexpr int target = 256;
+    const int per = target / split + (k < target % split ? 1 : 0);
+    const int64_t nblocks = (ts.rows + 15) / 16;
+    return int(std::max<int64_t>(1, std::min<int64_t>(std::min(per / lsqc_parts(ts.cols), kLsqpMaxGroups), nblocks)));
+  }
+  bool lsqc_fits(const std::vector<int64_t>& ranks, const LsqpBatch& b, int share) const {
+    const int split = std::max(b.ntasks, share > 0 ? share : lsqb_share());
+    for (size_t k = 0; k < ranks.size(); ++k) {
+      const TaskSpec& ts = tasks_[size_t(ranks[k] - 1)];
+      const int64_t nblocks = (ts.rows + 15) / 16;
+      const int ng = lsqc_groups(ts, split, int(k));
+      if ((nblocks + ng - 1) / ng > kLsqcMaxBlocks || !w_[size_t(ranks[k] - 1)].lsqc_xg) return false;
+    }
+    return true;
+  }
+  void build_lsqc(const std::vector<int64_t>& ranks, int share, LsqbLaunch& L) {
+    LsqpBatch& b = L.halves;
+    L.cpair = true;
+    const int split = std::max(b.ntasks, share > 0 ? share : lsqb_share());
+    int wgs = 0;
+    for (int k = 0; k < b.ntasks; ++k) {
+      const int64_t rank = ranks[size_t(k)];
+      const HipWorker& w = w_[size_t(rank - 1)];
+      const TaskSpec& ts = tasks_[size_t(rank - 1)];
+      LsqpTask& t = b.t[k];
+      t.xg = w.lsqc_xg;
+      t.parts = lsqc_parts(ts.cols);
+      b.grp0[k] = wgs;
+      wgs += lsqc_groups(ts, split, k) * t.parts;
+    }
+    b.grp0[b.ntasks] = wgs;
+    b.tick = w_[size_t(ranks[0] - 1)].lsqp_ctr + 2 * 8 * kLsqpCtrPerSlice + 4;
+    b.pfd = lsqc_la_;  // lsqc: the phase-1 lookahead
+    b.err = err_dev_;
+    b.spin_ticks = spin_ticks();
   }
 
   // the iterate-quarter single pass (lsqq_kernel.hip): cols <= 2048 on every task
@@ -1690,6 +1745,7 @@ class HipComm final : public Comm {
         pairs += ng;
       }
       b.grp0[b.ntasks] = pairs;
+      if (lsqc_ && lsqc_fits(ranks, b, share)) build_lsqc(ranks, share, L);
       return L;
     }
     if (lsqq_enabled(ranks)) {
@@ -1834,10 +1890,10 @@ class HipComm final : public Comm {
       HIPCHECK(hipEventRecord(tl.start, s));
     }
 #if MPA_MEASURE
-    HIPCHECK(b.pair ? (b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
+    HIPCHECK(b.pair ? (b.cpair ? launch_lsqc(b.halves, s) : b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
                     : b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #else
-    HIPCHECK(b.pair ? (b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
+    HIPCHECK(b.pair ? (b.cpair ? launch_lsqc(b.halves, s) : b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
                     : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #endif
     if (timed) {
@@ -2037,6 +2093,8 @@ class HipComm final : public Comm {
   bool may_hold_ = false;   // this call's wait completes without the held tasks (set_wait_hold)
   std::vector<int64_t> held_;  // held re-dispatches, launched with the next batch
   bool lsqp8_ = false;  // MPA_LSQP=8: the eight-wave single pass (lsqp_kernel.hip)
+  bool lsqc_ = false;   // MPA_LSQP=c: the column-pair single pass (lsqc_kernel.hip)
+  int lsqc_la_ = 1;     // MPA_LSQC_LA: its phase-1 lookahead in blocks (1 or 2)
   // lsqp L2 prefetch lead in blocks (MPA_LSQP_PF; 0 = off; unset: 1 for lsqp4, 0 for the
   // eight-wave cut).  lsqp4: 1 block 8.47 ms vs 9.50 without, 2-4 slower (L2 thrash);
   // profiles/r02_c5_lsqp_tuning.txt

@@ -194,14 +194,17 @@ def test_lsqb_descent_native_loop_matches_python_loop(M, monkeypatch, env):
     assert float(torch.linalg.norm(outs[0][0])) > 0
 
 
-@pytest.mark.parametrize("env", [{}, {"MPA_LSQP": "8"}, {"MPA_LSQP": "0"}, {"MPA_LSQF": "1"},
+@pytest.mark.parametrize("env", [{}, {"MPA_LSQP": "c"}, {"MPA_LSQP": "8"}, {"MPA_LSQP": "0"}, {"MPA_LSQF": "1"},
                                  {"MPA_LSQF": "1", "MPA_LSQF_DBG": "7"}, {"MPA_LSQQ": "1"}],
-                         ids=["lsqp4_pairs_default", "lsqp_eight_waves", "two_pass", "lsqf_xcd_local_groups",
-                              "lsqf_cross_xcd_groups", "lsqq_quads"])
-@pytest.mark.parametrize("rows,cols,n", [(1, 32, 1), (4113, 544, 1), (3000, 2048, 3), (20000, 1024, 2)])
+                         ids=["lsqp4_pairs_default", "lsqc_column_pairs", "lsqp_eight_waves", "two_pass",
+                              "lsqf_xcd_local_groups", "lsqf_cross_xcd_groups", "lsqq_quads"])
+@pytest.mark.parametrize("rows,cols,n", [(1, 32, 1), (4113, 544, 1), (3000, 2048, 3), (20000, 1024, 2),
+                                         (2500, 1312, 2)])
 def test_single_pass_vs_oracle(M, monkeypatch, env, rows, cols, n):
     """Every c5 kernel against the oracle: the default single pass by iterate halves
-    (lsqp4_kernel.hip: pairs of workgroups of one wave per SIMD, no exchange), the same
+    (lsqp4_kernel.hip: pairs of workgroups of one wave per SIMD, no exchange), column pairs
+    (lsqc_kernel.hip, MPA_LSQP=c: members split the columns and exchange per-block partial
+    products as tagged granules; one workgroup per row group at <= 1024 columns), the same
     scheme cut into eight waves (lsqp_kernel.hip, MPA_LSQP=8), the two passes (MPA_LSQP=0), and
     the opt-in single pass lsqf_kernel.hip (MPA_LSQF=1),
     groups of P = ceil(cols / 512) workgroups exchanging partial residuals inside an XCD
