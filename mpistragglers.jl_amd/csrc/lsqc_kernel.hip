@@ -44,6 +44,10 @@
 #include "kernels.hpp"
 #include "mpiasyncpools.h"
 
+#ifndef MPA_MEASURE
+#define MPA_MEASURE 0
+#endif
+
 namespace mpa {
 namespace {
 
@@ -52,6 +56,7 @@ using namespace dev;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int K = kLsqbIterates;   // 64 iterates
@@ -73,8 +78,7 @@ constexpr int XS = BROW + 16;      // X staging row stride
 constexpr int RS = 32 * 2 + 16;    // residual image row stride: k 0..31 bf16 + pad
 constexpr int XR = kLsqcXR;
 constexpr int PF = 4;              // G tree fan-in
-constexpr int DMA_W = 16;          // DMA instructions per block of waves 1 and 2
-constexpr int DMA_B = 2;           // ... of wave 3 (B)
+constexpr int DMA_W = 17;          // DMA instructions per block of waves 1 and 2 (16 of A, 1 of B)
 static_assert(CM == kLsqcMemberCols && 2 * CM == kLsqpMaxCols, "4 waves x 256 columns per member");
 static_assert(XR >= 4, "a member runs at most 3 blocks ahead of its partner's reads");
 
@@ -134,7 +138,9 @@ __device__ __forceinline__ f32x4 ld_wt(const f32x4* p) {
 
 // LA: phase 1 runs LA blocks ahead of phase 2 (the exchange has LA steps to land; DMA read-ahead
 // NS - 1 - LA blocks beyond the block phase 1 needs)
-template <int LA>
+// PR: phase probes, compile-time (measurement build only): 1 no A DMA, 2 no exchange, 8 no
+// phase-1 MFMAs, 32 no phase-2 MFMAs
+template <int LA, int PR>
 __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
   static_assert(LA >= 1 && LA <= 2, "lookahead");
   __shared__ __attribute__((aligned(16))) uint8_t ring[NS][SLOT];
@@ -159,7 +165,12 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
   while (ti + 1 < batch.ntasks && ticket >= batch.grp0[ti + 1]) ++ti;
   const LsqpTask& a = batch.t[ti];
   if (disarmed(a.go, a.seq)) return;  // every workgroup of the task alike
+  // phase probes (measurement build): 1 no A DMA, 2 no exchange, 8 no phase-1 MFMAs, 32 no phase-2 MFMAs
+  constexpr bool no_dma = PR & 1, no_x = PR & 2, no_p1 = PR & 8, no_p2 = PR & 32;
+  constexpr bool no_pub = PR & 4, no_poll = PR & 16, count_polls = PR & 64, late_pub = PR & 128, dma_at_c = PR & 256;
+  unsigned repolls = 0;
   const int P = a.parts;
+  const bool xchg = P == 2 && !no_x;  // the members exchange partial products
   const int j = ticket - batch.grp0[ti];
   const int q = j / P, h = j % P;
   const int ng = (batch.grp0[ti + 1] - batch.grp0[ti]) / P;
@@ -225,35 +236,39 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
     const int col = cs0 + CW * k + 8 * (pos ^ swz(2 * e + hi_row));
     return uint32_t(col < cols ? col : 0) * 2u;
   };
+  const uint32_t boff = uint32_t((lane >> 3) * BROW + (lane & 7) * 16);
   auto dma = [&](int64_t kb, int slot) __attribute__((always_inline)) {
     const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
     const int64_t r0 = kc * PRB;
     if (w == 1 || w == 2) {
       uint8_t* base = &ring[slot][0] + (w == 2 ? 2 * SUB : 0);
+      // B rows 8 (w - 1) .. + 7: lane l row l / 8, 16-B piece l % 8
+      const int eb = w - 1;
       if (r0 + PRB <= rows) {
-        const uint16_t* p = A + r0 * lda;
+        if (!no_dma) {
+          const uint16_t* p = A + r0 * lda;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          dma1k(p, coff(0, e) + row_b, base + 2 * e * ROWB);
-          dma1k(p, coff(1, e) + row_b, base + SUB + 2 * e * ROWB);
-          p += 2 * lda;
+          for (int e = 0; e < 8; ++e) {
+            dma1k(p, coff(0, e) + row_b, base + 2 * e * ROWB);
+            dma1k(p, coff(1, e) + row_b, base + SUB + 2 * e * ROWB);
+            p += 2 * lda;
+          }
         }
+        dma1k(Bm + (r0 + 8 * eb) * K, boff, &bring[slot][0] + eb * 1024);
       } else {  // a ragged last block: rows past the end re-read the last row (R = 0 there)
         const int nv = int(rows - r0);
+        if (!no_dma) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int row = 2 * e + hi_row;
-          const uint8_t* rp = reinterpret_cast<const uint8_t*>(A + (r0 + (row < nv ? row : nv - 1)) * lda);
-          dma16(rp + coff(0, e), base + 2 * e * ROWB);
-          dma16(rp + coff(1, e), base + SUB + 2 * e * ROWB);
+          for (int e = 0; e < 8; ++e) {
+            const int row = 2 * e + hi_row;
+            const uint8_t* rp = reinterpret_cast<const uint8_t*>(A + (r0 + (row < nv ? row : nv - 1)) * lda);
+            dma16(rp + coff(0, e), base + 2 * e * ROWB);
+            dma16(rp + coff(1, e), base + SUB + 2 * e * ROWB);
+          }
         }
-      }
-    } else if (w == 3) {
-#pragma unroll
-      for (int e = 0; e < DMA_B; ++e) {
-        int64_t row = r0 + 8 * e + (lane >> 3);
+        int64_t row = r0 + 8 * eb + (lane >> 3);
         row = row < rows ? row : rows - 1;
-        dma16(Bm + row * K + 8 * (lane & 7), &bring[slot][0] + e * 1024);
+        dma16(Bm + row * K + 8 * (lane & 7), &bring[slot][0] + eb * 1024);
       }
     }
   };
@@ -295,7 +310,8 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
     for (int s = 0; s < NKS; ++s) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) p1[t] = mfma(af[s % AD], XF[s][t], p1[t]);
+      for (int t = 0; t < NT; ++t)
+        if (!no_p1) p1[t] = mfma(af[s % AD], XF[s][t], p1[t]);
       if (s + AD < NKS) af[s % AD] = rd1(s + AD);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -307,34 +323,46 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
     for (int ww = 1; ww < QW; ++ww) Qw += part[ww][w][lane];
   };
   // wave 3 publishes block v's P_h, all four tiles (summed in wave order, as each wave's Qw)
-  // as soon as phase 1 is reduced.  Its stores share vmcnt with its B DMAs; the barrier-A wait
-  // counts only the younger B loads, which is safe whatever order stores retire in (loads
-  // retire in order: with at most DMA_B outstanding, the older B block has landed)
-  auto publish = [&](int v, const f32x4& Q3) __attribute__((always_inline)) {
-    const unsigned long long tg = (unsigned long long)(tag0 + uint32_t(v)) << 32;
+  // as soon as phase 1 is reduced.  Wave 3 issues no other vector memory op in the block loop
+  // and never waits on vmcnt there, so the write-through stores drain in the background
+  auto pub_sum = [&](const f32x4& Q3, f32x4 (&ps)[NT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      f32x4 s = Q3;
+      ps[t] = Q3;
       if (t != 3) {
-        s = part[0][t][lane];
+        ps[t] = part[0][t][lane];
 #pragma unroll
-        for (int ww = 1; ww < QW; ++ww) s += part[ww][t][lane];
+        for (int ww = 1; ww < QW; ++ww) ps[t] += part[ww][t][lane];
       }
-      unsigned long long* d = gslot(h, v) + (size_t(t) * 64 + lane) * 4;
+    }
+  };
+  // ... and stores them later (after barrier D, under phase 2, so that the stores' issue,
+  // which queues behind the block DMAs in the CU's memory pipeline, delays no barrier): lane's
+  // granules (t, lane, 0..3) as two 16-B write-through stores (a torn 16-B store still leaves
+  // whole 8-B {value, tag} granules, each checked by the reader)
+  auto pub_store = [&](int v, const f32x4 (&ps)[NT]) __attribute__((always_inline)) {
+    if (no_pub) return;
+    const uint32_t tg = tag0 + uint32_t(v);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        __hip_atomic_store(d + r, tg | __float_as_uint(s[r]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int t = 0; t < NT; ++t) {
+      unsigned long long* d = gslot(h, v) + (size_t(t) * 64 + lane) * 4;
+      const u32x4 lo = u32x4{__float_as_uint(ps[t][0]), tg, __float_as_uint(ps[t][1]), tg};
+      const u32x4 hi = u32x4{__float_as_uint(ps[t][2]), tg, __float_as_uint(ps[t][3]), tg};
+      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(lo) : "memory");
+      asm volatile("global_store_dwordx4 %0, %1, off offset:16 sc1" ::"v"(d), "v"(hi) : "memory");
     }
   };
   // wave 0: the partner's granules of block u -> gimg by LDS-DMA (write-through loads: L1 may
   // hold an older copy of the slot), 8 x 1 KiB
   auto poll_issue = [&](int u) __attribute__((always_inline)) {
+    if (no_poll) return;
     const uint8_t* src = reinterpret_cast<const uint8_t*>(gslot(1 - h, u)) + 16 * lane;
 #pragma unroll
     for (int k = 0; k < 8; ++k) dma16_sc1(src + 1024 * k, gimg + 1024 * k);
   };
   // ... wait for it, re-polling until every tag is block u's (bounded)
   auto poll_wait = [&](int u) __attribute__((always_inline)) {
+    if (no_poll) return;
     const uint32_t want = tag0 + uint32_t(u);
     const unsigned long long t0 = rt_now();
     for (unsigned k = 1;; ++k) {
@@ -345,7 +373,8 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
         const uint4 v = *reinterpret_cast<const uint4*>(gimg + 1024 * e + 16 * lane);
         ok &= v.y == want && v.w == want;
       }
-      if (__all(ok) || failed) break;
+      if (__all(ok) || failed || no_pub) break;
+      ++repolls;
       if ((k & 63) == 0 && rt_now() - t0 > ticks) {
         if (lane == 0) __hip_atomic_fetch_or(batch.err, 16u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         failed = true;
@@ -366,7 +395,6 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
 #pragma unroll
   for (int k = 0; k < NS - 1; ++k) dma(kb0 + k, k);
   if (w == 1 || w == 2) vm_wait<(NS - 1 - LA) * DMA_W>();
-  else if (w == 3) vm_wait<(NS - 1 - LA) * DMA_B>();
   barrier();
   f32x4 Qs[LA];  // this wave's tile of P_h for blocks u .. u + LA - 1
 #pragma unroll
@@ -375,35 +403,42 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
     Qs[k] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (k < nb) {
       phase1(k % NS, Qs[k]);
-      if (P == 2 && w == 3) publish(k, Qs[k]);
+      if (xchg && w == 3) {
+        f32x4 ps[NT];
+        pub_sum(Qs[k], ps);
+        pub_store(k, ps);
+      }
     }
   }
 
   uint8_t* rimg = reinterpret_cast<uint8_t*>(&part[0][0][0]);
+  if (xchg && w == 0) poll_issue(0);
   for (int u = 0; u < nb; ++u) {
     const int sl = u % NS;
     const bool more = u + LA < nb;
-    // wave 0: poll the partner's P(u) now; it is consumed after this step's phase 1
-    if (P == 2 && w == 0) poll_issue(u);
     // A: block u + LA landed (the DMAs of blocks u + LA + 1 .. u + NS - 2 are younger; waves
-    // 1-2 issue no other vector memory op, wave 3's granule stores: see publish)
+    // 1-2 issue no other vector memory op)
     if (w == 1 || w == 2) vm_wait<(NS - 2 - LA) * DMA_W>();
-    else if (w == 3) vm_wait<(NS - 2 - LA) * DMA_B>();
     barrier();
-    dma(kb0 + u + NS - 1, (u + NS - 1) % NS);
+    if (!dma_at_c) dma(kb0 + u + NS - 1, (u + NS - 1) % NS);
     f32x4 Qn = f32x4{0.f, 0.f, 0.f, 0.f};
     if (more) phase1((u + LA) % NS, Qn);
-    if (P == 2 && w == 3 && more) publish(u + LA, Qn);
+    f32x4 ps[NT];
+    if (xchg && w == 3 && more) {
+      pub_sum(Qn, ps);
+      if (!late_pub) pub_store(u + LA, ps);
+    }
     // wave 0 (no other vector memory op): the partner's P(u) in gimg
-    if (P == 2 && w == 0) poll_wait(u);
+    if (xchg && w == 0) poll_wait(u);
     const f32x4 Qk = Qs[0];
 #pragma unroll
     for (int k = 0; k + 1 < LA; ++k) Qs[k] = Qs[k + 1];
     Qs[LA - 1] = Qn;
     barrier();  // C: the partner's P in LDS; every wave done reading `part` (the image aliases it)
+    if (dma_at_c) dma(kb0 + u + NS - 1, (u + NS - 1) % NS);
     {
       f32x4 v = Qk;
-      if (P == 2) {  // the partner's tile w: values of granules (w, lane, 0..3)
+      if (xchg) {  // the partner's tile w: values of granules (w, lane, 0..3)
         const uint4 g0 = *reinterpret_cast<const uint4*>(gimg + (w * 64 + lane) * 32);
         const uint4 g1 = *reinterpret_cast<const uint4*>(gimg + (w * 64 + lane) * 32 + 16);
         v += f32x4{__uint_as_float(g0.x), __uint_as_float(g0.z), __uint_as_float(g1.x), __uint_as_float(g1.z)};
@@ -426,6 +461,10 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
       *reinterpret_cast<uint2*>(e + 32) = make_uint2(lw[0], lw[1]);
     }
     barrier();  // D
+    // wave 0: every wave has read gimg: poll the partner's P(u + 1) now, a step ahead of its use
+    // (its publish was LA - 1 steps before this one), under this step's phase 2
+    if (xchg && w == 0 && u + 1 < nb) poll_issue(u + 1);
+    if (late_pub && xchg && w == 3 && more) pub_store(u + LA, ps);
     // ---- phase 2: G_w^T[it][col] += sum_k R-image[it][k] A[row(k)][col]
     bf16x8 RF[NT];
 #pragma unroll
@@ -453,12 +492,15 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
         const bf16x8 bt =
             __builtin_bit_cast(bf16x8, __builtin_shufflevector(tb[c & 1][k][0], tb[c & 1][k][1], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-        for (int t = 0; t < NT; ++t) G[t][CH * c + k] = mfma(RF[t], bt, G[t][CH * c + k]);
+        for (int t = 0; t < NT; ++t)
+          if (!no_p2) G[t][CH * c + k] = mfma(RF[t], bt, G[t][CH * c + k]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
   drain_vm();  // the trailing (unused) DMA pieces and the last granule stores
+  if (count_polls && w == 0 && lane == 0 && ticket < 4)
+    printf("lsqc ticket %d: %u re-polls over %d blocks\n", ticket, repolls, nb);
 
   // ---- G over the row groups: fan-in-PF tree per (member, wave) of write-through partials
   const int nct = 2 * nks;
@@ -532,8 +574,20 @@ __global__ void __launch_bounds__(QT, 1) lsqc_kernel(LsqpBatch batch) {
 hipError_t launch_lsqc(const LsqpBatch& a, hipStream_t s) {
   const int wgs = a.grp0[a.ntasks];
   if (wgs <= 0 || !a.tick) return hipErrorInvalidValue;
-  if (a.pfd == 2) hipLaunchKernelGGL(lsqc_kernel<2>, dim3(wgs), dim3(QT), 0, s, a);
-  else hipLaunchKernelGGL(lsqc_kernel<1>, dim3(wgs), dim3(QT), 0, s, a);
+#if MPA_MEASURE
+#define MPA_LSQC_PROBE(pr)                                                                     \
+  if (a.dbg == pr) {                                                                         \
+    if (a.pfd == 2) hipLaunchKernelGGL((lsqc_kernel<2, pr>), dim3(wgs), dim3(QT), 0, s, a);  \
+    else hipLaunchKernelGGL((lsqc_kernel<1, pr>), dim3(wgs), dim3(QT), 0, s, a);             \
+    return hipGetLastError();                                                                \
+  }
+  MPA_LSQC_PROBE(1) MPA_LSQC_PROBE(2) MPA_LSQC_PROBE(3) MPA_LSQC_PROBE(40) MPA_LSQC_PROBE(42)
+  MPA_LSQC_PROBE(43) MPA_LSQC_PROBE(8) MPA_LSQC_PROBE(32) MPA_LSQC_PROBE(4) MPA_LSQC_PROBE(16)
+  MPA_LSQC_PROBE(20) MPA_LSQC_PROBE(64) MPA_LSQC_PROBE(128) MPA_LSQC_PROBE(256)
+#undef MPA_LSQC_PROBE
+#endif
+  if (a.pfd == 2) hipLaunchKernelGGL((lsqc_kernel<2, 0>), dim3(wgs), dim3(QT), 0, s, a);
+  else hipLaunchKernelGGL((lsqc_kernel<1, 0>), dim3(wgs), dim3(QT), 0, s, a);
   return hipGetLastError();
 }
 

@@ -341,7 +341,7 @@ class HipComm final : public Comm {
       lsqp8_ = e && *e == '8';
       lsqc_ = e && *e == 'c';
       const char* la = std::getenv("MPA_LSQC_LA");
-      lsqc_la_ = la && *la == '2' ? 2 : 1;
+      lsqc_la_ = la && *la == '1' ? 1 : 2;
     }
     hold_ok_ = !env_off("MPA_HOLD");
     if (const char* e = std::getenv("MPA_LSQP_PF")) lsqp_pfd_ = std::max(0, std::min(8, std::atoi(e)));
@@ -1247,7 +1247,15 @@ class HipComm final : public Comm {
       HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqp_ctr), sizeof(uint32_t) * nctr));
       HIPCHECK(hipMemset(w.lsqp_ctr, 0, sizeof(uint32_t) * nctr));
       const size_t xg = size_t(kLsqpMaxGroups) * 2 * kLsqcXR * 4 * 64 * 4 * sizeof(unsigned long long);
-      HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqc_xg), xg));
+      // the column pairs' exchange ring is rewritten every kLsqcXR blocks: in coarse-grained
+      // memory a reader's XCD L2 keeps serving its stale copy of a slot (sc1 loads bypass only
+      // L1), so the granules live in uncached device memory (MPA_LSQC_XG=fine / coarse: A/B)
+      {
+        const char* e = std::getenv("MPA_LSQC_XG");
+        const unsigned fl = e && !std::strcmp(e, "fine") ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
+        if (e && !std::strcmp(e, "coarse")) HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqc_xg), xg));
+        else HIPCHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&w.lsqc_xg), xg, fl));
+      }
       HIPCHECK(hipMemset(w.lsqc_xg, 0, xg));
       HIPCHECK(hipDeviceSynchronize());
     }
@@ -2094,7 +2102,7 @@ class HipComm final : public Comm {
   std::vector<int64_t> held_;  // held re-dispatches, launched with the next batch
   bool lsqp8_ = false;  // MPA_LSQP=8: the eight-wave single pass (lsqp_kernel.hip)
   bool lsqc_ = false;   // MPA_LSQP=c: the column-pair single pass (lsqc_kernel.hip)
-  int lsqc_la_ = 1;     // MPA_LSQC_LA: its phase-1 lookahead in blocks (1 or 2)
+  int lsqc_la_ = 2;     // MPA_LSQC_LA: its phase-1 lookahead in blocks (2; 1 for A/B)
   // lsqp L2 prefetch lead in blocks (MPA_LSQP_PF; 0 = off; unset: 1 for lsqp4, 0 for the
   // eight-wave cut).  lsqp4: 1 block 8.47 ms vs 9.50 without, 2-4 slower (L2 thrash);
   // profiles/r02_c5_lsqp_tuning.txt
