@@ -17,16 +17,20 @@
 // 512 w + 511 in both products:
 //   X_h slice   [512 cols x 32 its] as MFMA B operands XF[k-step][iterate tile]      (128)
 //   G partial   [512 cols x 32 its] fp32 accumulators G[iterate tile][column tile]   (256)
-//   A slice     [16 rows x 512 cols] of each block, by the wave's own LDS-DMA (one 1-KiB
-//               row per instruction) into a private 2-slot ring of 16 KiB slots, 16-B chunks
-//               XOR-swizzled per row (swz below) so that the row reads of phase 1 and the
-//               transposed reads of phase 2 are bank-conflict free
+//   A slice     [16 rows x 512 cols] of each block, by the wave's own LDS-DMA into a private
+//               2-slot ring of 16 KiB slots, each slot 8 strips of 64 columns (one DMA
+//               instruction = 8 rows x 128 B of a strip), 16-B chunks XOR-swizzled per row
+//               (sw below) so that the row reads of phase 1 and the transposed reads of
+//               phase 2 are bank-conflict free
 // Per block of 16 rows:
 //   phase 1   P_w = A[rows, cols_w] X_h[cols_w, :]    16 x 32, split-K over the 4 waves
-//   reduce    R = sum_w P_w (wave order) - B, bf16 hi + lo; each wave reduces a quarter  2 barriers
+//   reduce    R = sum_w P_w (wave order; wave 0 starts from -B), bf16 hi + lo, one barrier: every
+//             wave sums all of R and moves it into phase 2's operand layout by lane swaps
 //   phase 2   G_w^T += R^T A[rows, cols_w]   one K = 32 MFMA per tile: k 0-15 the hi residual
 //             of rows 0-15, k 16-31 the lo residual of the same rows; A^T by ds_read_b64_tr_b16
-// The DMA of block u + 2 is issued once phase 2 of block u has read its slot.
+// The DMA of block u + 2 goes out strip by strip inside phase 2 of block u, as each strip's
+// column tiles are read (the DMA issue runs beside MFMAs and a strip's lead is ~1.5 blocks of
+// compute); phase 1 of a block waits for it strip by strip.
 //
 // G over the row groups of a half: each wave's partial is stored write-through and summed
 // by a fan-in-4 tree per (half, wave) in group order (the last arriver of a group carries it
@@ -41,9 +45,6 @@
 #include "kernels.hpp"
 #include "mpiasyncpools.h"
 
-#ifndef MPA_MEASURE
-#define MPA_MEASURE 0
-#endif
 
 namespace mpa {
 namespace {
@@ -67,17 +68,15 @@ constexpr int NCT = QKW / 16;         // column tiles of phase 2 (32)
 constexpr int PH = 32;                // iterates per workgroup (one half)
 constexpr int SLICE = PRB * ROWB;     // 16 KiB
 constexpr int XS = PH * 2 + 16;       // X staging row stride (bytes)
-constexpr int RS = 32 * 2 + 16;       // residual image row stride: k 0..31 bf16 + pad
 constexpr int PF = 4;                 // G tree fan-in
 static_assert(QW * QKW == kLsqpMaxCols, "4 waves x 512 columns");
+static_assert(NKS == 16 && NCT == 32, "8 strips of 64 columns per wave");
 
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ uint16_t bf16_rne(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return uint16_t((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
-}
+// round to nearest even by the hardware's conversion (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint16_t bf16_cvt(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 __device__ __forceinline__ float bf16_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xc07f); }  // lgkmcnt(0)
 // workgroup barrier that leaves the vector-memory queue alone (the next block's DMA stays in
@@ -102,9 +101,10 @@ __device__ __forceinline__ void dma16(const void* src, void* lds) {
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(l) : "memory", "m0");
 }
 
-// 16-B chunk c of slice row r sits at chunk position c ^ swz(r) (bits 1-3 only, so 256-B
-// groups of chunks stay put and k-steps / column tiles 4 (8) apart are immediate offsets)
-__host__ __device__ constexpr int swz(int r) { return 2 * (r & 3) + (r & 8); }
+// 16-B chunk c of strip row r sits at chunk position c ^ sw(r) (bits 1-2 only: chunk pairs
+// stay together); found by search over the linear maps of r's bits for conflict-free reads of
+// both phases (tools/lsqp4_swizzle.py)
+__host__ __device__ constexpr int sw(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
 
 // write-through 16-B store / load as two 8-B agent-scope accesses (the G tree's hand-off:
 // MI355X_MICROARCH.md §inter-workgroup visibility, "one lane adds for the producer, the last
@@ -126,8 +126,9 @@ __device__ __forceinline__ f32x4 ld_wt(const f32x4* p) {
 __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[QW][2][SLICE];
   __shared__ __attribute__((aligned(16))) uint8_t bring[2][PRB * PH * 2];
-  __shared__ __attribute__((aligned(16))) f32x4 part[QW][2][64];
-  __shared__ __attribute__((aligned(16))) uint8_t rimg[2 * 16 * RS];
+  // phase-1 partials, double-buffered by block parity: with one barrier per block, a wave
+  // may store block u + 1's partial while a slower wave still reads block u's
+  __shared__ __attribute__((aligned(16))) f32x4 part[2][QW][2][64];
   __shared__ __attribute__((aligned(16))) uint32_t sink[QW][64];
 
   // blocks b and b + 8 are the two halves of one pair (one XCD under round-robin placement;
@@ -193,58 +194,80 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   }
 
   // ---- the wave's DMA of block kb (clamped: past the range it re-reads the range's last
-  // block into the free slot, unused, so every step issues the same number of loads).
-  // Row e of the slice is one instruction; lane l loads logical chunk l ^ swz(e), stored at
-  // position l.  Chunks past cols load column 0 (never used).
+  // block into the free slot, unused, so every step issues the same number of loads)
   const int64_t lda = a.lda;
-  uint32_t voff[8];  // byte offset in the row, per distinct swizzle 2 * s8
+  // ---- the strip ring.  A wave's slice of a block (16 rows x 512 columns) is 8 strips of 64
+  // columns; strip k (2 KiB) sits at k * 2048, row r of it (128 B) at r * 128, logical 16-B
+  // chunk c of the row at position c ^ sw(r): bank-conflict free for phase 1's row reads and
+  // phase 2's transposed reads.  One DMA instruction moves half a strip (8 rows x 128 B; lane l:
+  // row 8j + l / 8, position l % 8), so phase 2 hands a strip back as soon as its four column
+  // tiles are read, and phase 1 waits for a block strip by strip.
+  // Per-lane offsets from the block's first row at column c0: strip half j, a full strip or
+  // one whose last 32 columns lie past cols (cols % 32 == 0; those lanes re-read the first 32)
+  uint32_t vfull[2], vpart[2];
+  auto voffs = [&](int nv, uint32_t (&vf)[2], uint32_t (&vp)[2]) __attribute__((always_inline)) {
 #pragma unroll
-  for (int s8 = 0; s8 < 8; ++s8) {
-    const int c = lane ^ (2 * s8);
-    voff[s8] = uint32_t(c0 + 8 * c < cols ? c0 + 8 * c : 0) * 2u;
-  }
-  const bool no_dma = MPA_MEASURE && (batch.dbg & 1), no_compute = MPA_MEASURE && (batch.dbg & 2);
-  // phase probes (measurement build): 8 no phase 1, 16 no partials / reduce / barriers, 32 no phase 2
-  const bool no_p1 = MPA_MEASURE && (batch.dbg & 8), no_red = MPA_MEASURE && (batch.dbg & 16),
-             no_p2 = MPA_MEASURE && (batch.dbg & 32);
-  auto dma = [&](int64_t kb, uint8_t* slot) __attribute__((always_inline)) {
-    if (no_dma) return;
+    for (int j = 0; j < 2; ++j) {
+      const int pr = 8 * j + (lane >> 3);     // row position in the strip
+      const int rr = pr < nv ? pr : nv - 1;   // rows past the end re-read the last row (R = 0)
+      const int c = (lane & 7) ^ sw(pr);
+      const uint32_t rb = uint32_t(rr) * uint32_t(lda) * 2u;
+      vf[j] = rb + uint32_t(c) * 16u;
+      vp[j] = rb + uint32_t(c & 3) * 16u;
+    }
+  };
+  voffs(PRB, vfull, vpart);
+  struct Blk {
+    const uint16_t* p;  // first row of the block (clamped into the range)
+    int nv;             // valid rows
+  };
+  auto blk = [&](int64_t kb) __attribute__((always_inline)) {
     const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
     const int64_t r0 = kc * PRB;
-    const uint16_t* p = A + r0 * lda;
-    if (r0 + PRB <= rows) {  // every block but a ragged last one: one scalar add per row
+    return Blk{A + r0 * lda, int(rows - r0 < PRB ? rows - r0 : PRB)};
+  };
+  // strip k of a block into a slot: 2 instructions.  Strips wholly past cols load columns
+  // 0 .. 31 (finite data that meets X = 0; their G columns are never stored)
+  auto dma_strip = [&](const Blk& b, const uint32_t (&vf)[2], const uint32_t (&vp)[2], int k, uint8_t* slot)
+      __attribute__((always_inline)) {
+    const int cb = c0 + 64 * k;
+    const bool full = cb + 64 <= cols;
+    const uint16_t* base = b.p + (cb < cols ? cb : 0);
 #pragma unroll
-      for (int e = 0; e < PRB; ++e) {
-        dma_row(p, voff[swz(e) >> 1], slot + e * ROWB);
-        p += lda;
-      }
-    } else {  // rows past the end re-read the last row (they meet R = 0)
-      const int nv = int(rows - r0);
+    for (int j = 0; j < 2; ++j) dma_row(base, full ? vf[j] : vp[j], slot + 2048 * k + 1024 * j);
+  };
+  auto dma = [&](int64_t kb, uint8_t* slot) __attribute__((always_inline)) {
+    const Blk b = blk(kb);
+    uint32_t vf[2], vp[2];
+    voffs(b.nv, vf, vp);
 #pragma unroll
-      for (int e = 0; e < PRB; ++e) dma_row(p + (e < nv ? e : nv - 1) * lda, voff[swz(e) >> 1], slot + e * ROWB);
-    }
+    for (int k = 0; k < 8; ++k) dma_strip(b, vf, vp, k, slot);
   };
   // L2 prefetch of block kb: 4 B per lane into a per-wave sink nobody reads, a lane per 128-B
   // line; member h takes rows 8h .. 8h + 7 of the wave's slice (the pair shares the XCD's L2),
-  // so the DMA of the block, pfd steps later, finds its lines on chip
+  // so the DMA of the block, pfd steps later, finds its lines on chip.  Always issued (pfd = 0
+  // re-touches the block being loaded), so every wait counts the same loads
   const int pfd = batch.pfd;
   const uint32_t pfoff = uint32_t(c0 + 64 * (lane & 7) < cols ? c0 + 64 * (lane & 7) : 0) * 2u;
   auto pf = [&](int64_t kb) __attribute__((always_inline)) {
-    if (no_dma) return;
     const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
     int64_t row = kc * PRB + 8 * h + (lane >> 3);
     row = row < rows ? row : rows - 1;
     pf4(reinterpret_cast<const uint8_t*>(A + row * lda) + pfoff, &sink[w][0]);
   };
-  // B of a block (16 rows x 32 iterates of half h = 16 x 64 B: one instruction of wave 0)
+  // B of a block (16 rows x 32 iterates of half h = 16 x 64 B): one instruction of wave 0; the
+  // other waves touch the same rows into their sink instead, so every wave counts one load
   const int brow = lane >> 2, bpiece = lane & 3;
   auto dma_b = [&](int64_t kb, uint8_t* bslot) __attribute__((always_inline)) {
-    if (no_dma) return;
     const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
     int64_t row = kc * PRB + brow;
     row = row < rows ? row : rows - 1;
-    dma16(Bm + row * K + PH * h + 8 * bpiece, bslot);
+    const uint16_t* src = Bm + row * K + PH * h + 8 * bpiece;
+    if (w == 0) dma16(src, bslot);
+    else pf4(src, &sink[w][0]);
   };
+  // vmcnt(n) alone (expcnt / lgkmcnt fields left free)
+#define MPA_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
 
   f32x4 G[2][NCT];  // G^T tiles: [iterate tile][column tile], lane (i, g): its 4g + r, column i
 #pragma unroll
@@ -252,117 +275,133 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) G[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // step u DMAs block u + 2 and prefetches block u + 2 + pfd.  The prologue issues what steps
-  // -2 and -1 would have, so every step's wait counts the same loads; blocks 2 .. pfd - 1,
-  // which no step prefetches, go first (older than everything the waits count)
+  // step u issues block u + 2: B, its 8 strips (inside phase 2, as block u's strips are read),
+  // then the prefetch of block u + 2 + pfd.  The prologue issues what steps -2 and -1 would
+  // have, so every wait counts the same loads; blocks 2 .. pfd - 1, which no step prefetches,
+  // go first (older than everything the waits count)
   for (int d = 2; d < pfd; ++d) pf(kb0 + d);
+  dma_b(kb0, bring[0]);
   dma(kb0, my0);
-  if (w == 0) dma_b(kb0, bring[0]);
-  if (pfd) pf(kb0 + pfd);
+  pf(kb0 + pfd);
+  dma_b(kb0 + 1, bring[1]);
   dma(kb0 + 1, my1);
-  if (w == 0) dma_b(kb0 + 1, bring[1]);
-  if (pfd) pf(kb0 + 1 + pfd);
+  pf(kb0 + 1 + pfd);
 
-  // LDS offsets inside a slot: k-step s reads chunk 4s + g of row i; column tile ct reads
-  // chunks 2ct, 2ct + 1 of rows r0 and r0 + 4
-  int off1[4], off2[8];
+  // LDS offsets inside a slot: k-step s reads chunk 4 (s & 1) + g of row i of strip s / 2;
+  // column tile ct reads chunks 2 (ct & 3), +1 of rows r0 and r0 + 4 of strip ct / 4
+  int off1[2], off2[4];
 #pragma unroll
-  for (int s4 = 0; s4 < 4; ++s4) off1[s4] = i * ROWB + ((4 * s4 + g) ^ swz(i)) * 16;
+  for (int s2 = 0; s2 < 2; ++s2) off1[s2] = i * 128 + ((4 * s2 + g) ^ sw(i)) * 16;
   {
     const int r0 = 8 * (g & 1) + qq;
 #pragma unroll
-    for (int c8 = 0; c8 < 8; ++c8) off2[c8] = r0 * ROWB + (((2 * c8) ^ swz(r0)) + (p4 >> 1)) * 16 + 8 * (p4 & 1);
+    for (int c4 = 0; c4 < 4; ++c4) off2[c4] = r0 * 128 + ((2 * c4 + (p4 >> 1)) ^ sw(r0)) * 16 + 8 * (p4 & 1);
   }
-  // the reduce: wave w sums components 2 (w & 1), +1 of iterate tile w >> 1 (rows 4g + rr)
-  const int rt = w >> 1, rc = 2 * (w & 1);
 
-  auto step = [&](int u, uint8_t* slot, const uint8_t* bslot) __attribute__((always_inline)) {
-    // this block's DMA has landed: all but the youngest loads (the next block's 16 rows and
-    // wave 0's B piece) are done.  vmcnt(16) / vmcnt(17): expcnt / lgkmcnt fields left free
-    if (pfd) {  // + the two prefetches issued after this block's DMA: vmcnt(18) / vmcnt(19)
-      if (w == 0) __builtin_amdgcn_s_waitcnt(0x4F73);
-      else __builtin_amdgcn_s_waitcnt(0x4F72);
-    } else {
-      if (w == 0) __builtin_amdgcn_s_waitcnt(0x4F71);
-      else __builtin_amdgcn_s_waitcnt(0x4F70);
-    }
-    if (no_compute) {  // measurement: the DMA ring alone
-      lgkm_drain();
-      dma(kb0 + u + 2, slot);
-      if (w == 0) dma_b(kb0 + u + 2, const_cast<uint8_t*>(bslot));
-      if (pfd) pf(kb0 + u + 2 + pfd);
-      return;
-    }
+  auto step = [&](int u, uint8_t* slot, uint8_t* bslot, f32x4 (&pt)[QW][2][64]) __attribute__((always_inline)) {
     // ---- phase 1: P_w[rows 4g + r][iterate 16 t + i].  Fragment reads run eight k-steps
-    // ahead of the MFMAs (the compiler waits for each with a counted lgkmcnt)
+    // ahead of the MFMAs; strip k of this block has landed once at most the loads issued after
+    // it are pending: the rest of the block's strips (2 (7 - k)), its prefetch, and the next
+    // block's B, 16 strip loads and prefetch (18)
     constexpr int AD = 8;
+    MPA_VMCNT(2 * (7 - 3) + 19);  // strips 0-3 (and B, older)
     f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    if (!no_p1) {
+    if (w == 0) {  // wave 0 DMA'd B: its accumulators start at -B
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          p1[t][r] = -bf16_f32(*reinterpret_cast<const uint16_t*>(bslot + (4 * g + r) * (PH * 2) + 2 * (16 * t + i)));
+    }
+    {
     bf16x8 af[AD];
     auto rd1 = [&](int s) __attribute__((always_inline)) {
-      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + off1[s & 3] + 256 * (s >> 2)));
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + off1[s & 1] + 2048 * (s >> 1)));
     };
 #pragma unroll
     for (int s = 0; s < AD; ++s) af[s] = rd1(s);
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       __builtin_amdgcn_sched_barrier(0);
+      // before the reads of strip (s + 8) / 2 (s unrolled: one wait survives per even s)
+      if (s == 0) MPA_VMCNT(2 * (7 - 4) + 19);
+      if (s == 2) MPA_VMCNT(2 * (7 - 5) + 19);
+      if (s == 4) MPA_VMCNT(2 * (7 - 6) + 19);
+      if (s == 6) MPA_VMCNT(2 * (7 - 7) + 19);
       p1[0] = mfma(af[s % AD], XF[s][0], p1[0]);
       p1[1] = mfma(af[s % AD], XF[s][1], p1[1]);
       if (s + AD < NKS) af[s % AD] = rd1(s + AD);
     }
     __builtin_amdgcn_sched_barrier(0);
     }
-    if (!no_red) {
-    part[w][0][lane] = p1[0];
-    part[w][1][lane] = p1[1];
-    barrier();
-    // ---- reduce: R = sum_w P_w - B for rows 4g + rc, +1 of iterate 16 rt + i, as hi / lo
-    // into the phase-2 A-operand image rimg[t][i][k]: k = row (hi), 16 + row (lo)
-    {
-      f32x2 v = *reinterpret_cast<const f32x2*>(reinterpret_cast<const float*>(&part[0][rt][lane]) + rc);
-#pragma unroll
-      for (int ww = 1; ww < QW; ++ww)
-        v += *reinterpret_cast<const f32x2*>(reinterpret_cast<const float*>(&part[ww][rt][lane]) + rc);
-      const int64_t row0 = (kb0 + u) * PRB + 4 * g + rc;
-      const uint32_t b2 = *reinterpret_cast<const uint32_t*>(bslot + (4 * g + rc) * (PH * 2) + 2 * (16 * rt + i));
-      const uint32_t b3 = *reinterpret_cast<const uint32_t*>(bslot + (4 * g + rc + 1) * (PH * 2) + 2 * (16 * rt + i));
-      uint32_t hw = 0, lw = 0;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const float b = bf16_f32(uint16_t(e ? b3 : b2));
-        const float x = row0 + e < rows ? v[e] - b : 0.f;  // rows past the end: R = 0
-        const uint16_t hi = bf16_rne(x);
-        const uint16_t lo = bf16_rne(x - bf16_f32(hi));
-        hw |= uint32_t(hi) << (16 * e);
-        lw |= uint32_t(lo) << (16 * e);
-      }
-      uint8_t* e = rimg + (rt * 16 + i) * RS + 2 * (4 * g + rc);
-      *reinterpret_cast<uint32_t*>(e) = hw;
-      *reinterpret_cast<uint32_t*>(e + 32) = lw;
-    }
-    barrier();
-    }
-    // ---- phase 2: G_w^T[it][col] += sum_k R-image[it][k] A[row(k)][col]
-    bf16x8 RF[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-      RF[t] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(rimg + (t * 16 + i) * RS + 16 * g));
-    // column tiles in chunks of 4 (8 transposed reads), double-buffered: the reads of chunk
-    // c + 1 are issued before the MFMAs of chunk c
+    // phase 2's column tiles in chunks of 4 = one strip (8 transposed reads), double-buffered:
+    // the reads of chunk c + 1 are issued before the MFMAs of chunk c; chunk 0's go out before
+    // the reduce's barrier (they read only this wave's slot)
     constexpr int CH = 4;
     s16x4 tb[2][CH][2];
     auto rd = [&](int c, s16x4 (&d)[CH][2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
-        const int ct = CH * c + k;
-        const uint8_t* src = slot + off2[ct & 7] + 256 * (ct >> 3);
+        const uint8_t* src = slot + off2[k] + 2048 * c;
         d[k][0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(src));
-        d[k][1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(src + 4 * ROWB));
+        d[k][1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(src + 4 * 128));
       }
     };
-    if (!no_p2) {
     rd(0, tb[0]);
+    // ---- reduce, one barrier: every wave sums the four partials (wave order; wave 0's carry
+    // -B) into R in the accumulator layout (rows 4g + r, iterate 16t + i), splits it into bf16
+    // hi + lo, and moves the halves into phase 2's A operand with two lane swaps:
+    //   RF[t] lane (i, g) = k 8g .. 8g + 7 = hi rows 0-7 | hi 8-15 | lo 0-7 | lo 8-15 (g = 0..3)
+    // from lane groups' (H_g, L_g) = rows 4g .. 4g + 3: permlane32 (H, L) -> X = (H0 H1 L0 L1),
+    // Y = (H2 H3 L2 L3); permlane16 (X, Y) -> X = (H0 H2 L0 L2), Y = (H1 H3 L1 L3) = the first
+    // and second four k of every lane group
+    bf16x8 RF[2];
+    pt[w][0][lane] = p1[0];
+    pt[w][1][lane] = p1[1];
+    barrier();
+    {
+      const int64_t row0 = (kb0 + u) * PRB + 4 * g;
+      const bool ragged = (kb0 + u + 1) * PRB > rows;  // wave-uniform
+      f32x4 pv[2][QW];  // all eight reads in flight at once
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ww = 0; ww < QW; ++ww) pv[t][ww] = pt[ww][t][lane];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 v = pv[t][0];
+#pragma unroll
+        for (int ww = 1; ww < QW; ++ww) v += pv[t][ww];
+        if (ragged) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = row0 + r < rows ? v[r] : 0.f;  // rows past the end: R = 0
+        }
+        uint32_t H[2], L[2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const uint16_t h0 = bf16_cvt(v[2 * d]), h1 = bf16_cvt(v[2 * d + 1]);
+          const uint16_t l0 = bf16_cvt(v[2 * d] - bf16_f32(h0)), l1 = bf16_cvt(v[2 * d + 1] - bf16_f32(h1));
+          H[d] = uint32_t(h0) | uint32_t(h1) << 16;
+          L[d] = uint32_t(l0) | uint32_t(l1) << 16;
+        }
+        uint32_t X[2], Y[2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto sa = __builtin_amdgcn_permlane32_swap(H[d], L[d], false, false);
+          const auto sb = __builtin_amdgcn_permlane16_swap(sa[0], sa[1], false, false);
+          X[d] = sb[0];
+          Y[d] = sb[1];
+        }
+        RF[t] = __builtin_bit_cast(bf16x8, make_uint4(X[0], X[1], Y[0], Y[1]));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // chunk 1's reads stay behind the reduce (registers)
+    // ---- phase 2: G_w^T[it][col] += sum_k R-image[it][k] A[row(k)][col]; strip c of the slot
+    // is refilled with block u + 2's once chunk c's MFMAs have consumed its reads
+    dma_b(kb0 + u + 2, bslot);
+    const Blk nb2 = blk(kb0 + u + 2);
+    uint32_t vf[2] = {vfull[0], vfull[1]}, vp[2] = {vpart[0], vpart[1]};
+    if (nb2.nv < PRB) voffs(nb2.nv, vf, vp);
 #pragma unroll
     for (int c = 0; c < NCT / CH; ++c) {
       if (c + 1 < NCT / CH) rd(c + 1, tb[(c + 1) & 1]);
@@ -375,18 +414,15 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
         G[1][CH * c + k] = mfma(RF[1], bt, G[1][CH * c + k]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      dma_strip(nb2, vf, vp, c, slot);
     }
-    }
-    // the slot is read: DMA block u + 2 into it
-    lgkm_drain();
-    dma(kb0 + u + 2, slot);
-    if (w == 0) dma_b(kb0 + u + 2, const_cast<uint8_t*>(bslot));
-    if (pfd) pf(kb0 + u + 2 + pfd);
+    pf(kb0 + u + 2 + pfd);
   };
   for (int u = 0; u < nb; u += 2) {
-    step(u, my0, bring[0]);
-    if (u + 1 < nb) step(u + 1, my1, bring[1]);
+    step(u, my0, bring[0], part[0]);
+    if (u + 1 < nb) step(u + 1, my1, bring[1], part[1]);
   }
+#undef MPA_VMCNT
   drain_vm();  // the trailing (unused) DMA pieces
 
   // ---- G over the row groups: fan-in-PF tree per (half, wave) of write-through partials
