@@ -69,6 +69,12 @@ constexpr int PH = 32;                // iterates per workgroup (one half)
 constexpr int SLICE = PRB * ROWB;     // 16 KiB
 constexpr int XS = PH * 2 + 16;       // X staging row stride (bytes)
 constexpr int PF = 4;                 // G tree fan-in
+#ifndef MPA_LSQP4_P2L
+#define MPA_LSQP4_P2L 2               // phase-2 transposed-read chunks in flight ahead
+#endif
+#ifndef MPA_LSQP4_AD
+#define MPA_LSQP4_AD 4                // phase-1 fragment read-ahead in k-steps
+#endif
 static_assert(QW * QKW == kLsqpMaxCols, "4 waves x 512 columns");
 static_assert(NKS == 16 && NCT == 32, "8 strips of 64 columns per wave");
 
@@ -268,6 +274,21 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   };
   // vmcnt(n) alone (expcnt / lgkmcnt fields left free)
 #define MPA_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
+  // strip k of the current block has landed once at most the loads issued after it are
+  // pending: the rest of the block's strips (2 (7 - k)), its prefetch, and the next block's B,
+  // 16 strip loads and prefetch (18).  k is a constant after unrolling: one wait survives
+  auto wait_strip = [&](int k) __attribute__((always_inline)) {
+    switch (k) {
+      case 0: MPA_VMCNT(2 * 7 + 19); break;
+      case 1: MPA_VMCNT(2 * 6 + 19); break;
+      case 2: MPA_VMCNT(2 * 5 + 19); break;
+      case 3: MPA_VMCNT(2 * 4 + 19); break;
+      case 4: MPA_VMCNT(2 * 3 + 19); break;
+      case 5: MPA_VMCNT(2 * 2 + 19); break;
+      case 6: MPA_VMCNT(2 * 1 + 19); break;
+      default: MPA_VMCNT(19); break;
+    }
+  };
 
   f32x4 G[2][NCT];  // G^T tiles: [iterate tile][column tile], lane (i, g): its 4g + r, column i
 #pragma unroll
@@ -299,12 +320,10 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   }
 
   auto step = [&](int u, uint8_t* slot, uint8_t* bslot, f32x4 (&pt)[QW][2][64]) __attribute__((always_inline)) {
-    // ---- phase 1: P_w[rows 4g + r][iterate 16 t + i].  Fragment reads run eight k-steps
-    // ahead of the MFMAs; strip k of this block has landed once at most the loads issued after
-    // it are pending: the rest of the block's strips (2 (7 - k)), its prefetch, and the next
-    // block's B, 16 strip loads and prefetch (18)
-    constexpr int AD = 8;
-    MPA_VMCNT(2 * (7 - 3) + 19);  // strips 0-3 (and B, older)
+    // ---- phase 1: P_w[rows 4g + r][iterate 16 t + i].  Fragment reads run AD k-steps ahead
+    // of the MFMAs, each strip's after its wait
+    constexpr int AD = MPA_LSQP4_AD;
+    wait_strip((AD - 1) / 2);  // the strips of the first AD k-steps (and B, older)
     f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (w == 0) {  // wave 0 DMA'd B: its accumulators start at -B
 #pragma unroll
@@ -323,11 +342,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       __builtin_amdgcn_sched_barrier(0);
-      // before the reads of strip (s + 8) / 2 (s unrolled: one wait survives per even s)
-      if (s == 0) MPA_VMCNT(2 * (7 - 4) + 19);
-      if (s == 2) MPA_VMCNT(2 * (7 - 5) + 19);
-      if (s == 4) MPA_VMCNT(2 * (7 - 6) + 19);
-      if (s == 6) MPA_VMCNT(2 * (7 - 7) + 19);
+      if (s + AD < NKS && ((s + AD) & 1) == 0) wait_strip((s + AD) / 2);
       p1[0] = mfma(af[s % AD], XF[s][0], p1[0]);
       p1[1] = mfma(af[s % AD], XF[s][1], p1[1]);
       if (s + AD < NKS) af[s % AD] = rd1(s + AD);
@@ -338,7 +353,8 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     // the reads of chunk c + 1 are issued before the MFMAs of chunk c; chunk 0's go out before
     // the reduce's barrier (they read only this wave's slot)
     constexpr int CH = 4;
-    s16x4 tb[2][CH][2];
+    constexpr int P2L = MPA_LSQP4_P2L;  // chunks of reads in flight ahead of the MFMAs
+    s16x4 tb[P2L + 1][CH][2];
     auto rd = [&](int c, s16x4 (&d)[CH][2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
@@ -404,12 +420,16 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     if (nb2.nv < PRB) voffs(nb2.nv, vf, vp);
 #pragma unroll
     for (int c = 0; c < NCT / CH; ++c) {
-      if (c + 1 < NCT / CH) rd(c + 1, tb[(c + 1) & 1]);
+      if (c == 0) {
+#pragma unroll
+        for (int c2 = 1; c2 < P2L; ++c2) rd(c2, tb[c2]);
+      }
+      if (c + P2L < NCT / CH) rd(c + P2L, tb[(c + P2L) % (P2L + 1)]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
-        const bf16x8 bt =
-            __builtin_bit_cast(bf16x8, __builtin_shufflevector(tb[c & 1][k][0], tb[c & 1][k][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        const bf16x8 bt = __builtin_bit_cast(
+            bf16x8, __builtin_shufflevector(tb[c % (P2L + 1)][k][0], tb[c % (P2L + 1)][k][1], 0, 1, 2, 3, 4, 5, 6, 7));
         G[0][CH * c + k] = mfma(RF[0], bt, G[0][CH * c + k]);
         G[1][CH * c + k] = mfma(RF[1], bt, G[1][CH * c + k]);
       }
