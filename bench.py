@@ -412,11 +412,15 @@ def run_single(args, cfg):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     timing = comm.timing()
-    comm.set_timing(False)
     extra["exchange"] = exchange_report(comm.exchange_timing())
     fresh = int((pool.repochs == pool.epoch).sum())
+    # launches after the timed region (waitall releases held stale re-dispatches): counted, so
+    # that a kernel trace of this command can drop them from its timed-region window
+    # (tools/trace_window.py)
     M.waitall_(pool, recv, irecv)
     torch.cuda.synchronize()
+    extra["launches_after_timed"] = comm.timing()[0]
+    comm.set_timing(False)
     extra["measured_read_peak"] = read_peak(M, torch)
     extra.update({"x_norm": float(torch.linalg.norm(x.float()).item()), "build": M.lib().mpa_build_info().decode(),
                   "loop": "native coordinator loop (mpa_lsq%s_descent)" % ("b" if batched else ""),
