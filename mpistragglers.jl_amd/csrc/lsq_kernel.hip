@@ -58,7 +58,8 @@ struct Tile {
   P d[RB][VPL];
 
   // rows [base, base+RB): out-of-range rows/vectors either branch (default) or read a
-  // clamped in-bounds address (M_CLAMP) whose contribution is zeroed by x = 0 / res = 0
+  // clamped in-bounds address (M_CLAMP: the row's last valid row, vector 0 of the row for
+  // lanes past cols) whose contribution is zeroed by x = 0 / res = 0
   __device__ __forceinline__ void load(const T* A, int64_t base, int64_t rows, int64_t lda, int lane,
                                        const bool (&vok)[VPL]) {
 #pragma unroll
@@ -68,7 +69,7 @@ struct Tile {
         const int64_t r = r0 < rows ? r0 : rows - 1;
         const P* row = reinterpret_cast<const P*>(A + r * lda);
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) d[rb][v] = ld16<T, (MODE & M_NT) != 0>(row + (vok[v] ? v * 64 + lane : lane));
+        for (int v = 0; v < VPL; ++v) d[rb][v] = ld16<T, (MODE & M_NT) != 0>(row + (vok[v] ? v * 64 + lane : 0));
       } else {
         const P* row = reinterpret_cast<const P*>(A + r0 * lda);
 #pragma unroll

@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(kThreads) lsqw_grad_kernel(LsqBatch batch) {
       rr[rb] = ok ? r[rc] : T(0);
       const P* ar = reinterpret_cast<const P*>(A + rc * a.lda);
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) d[rb][v] = ld16<T, true>(ar + (vok[v] ? v * 64 + lane : lane));
+      for (int v = 0; v < VPL; ++v) d[rb][v] = ld16<T, true>(ar + (vok[v] ? v * 64 + lane : 0));
     }
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
