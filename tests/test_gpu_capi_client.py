@@ -7,8 +7,9 @@ for 16-B vectors past `cols` (lanes of the last vector group when cols < 64 vect
 at vector `lane` of the row instead of vector 0, past the end of A on the last row (fixed in
 lsq_kernel.hip / lsqw_kernel.hip).  Cases: narrow rows with a partial vector group (fp64 64
 columns, fp32 100 and 8), a full-width narrow row, wide rows with a one-vector last slice;
-1-3 workers; every reply against a host fp64 gradient of the device's own A and b
-(relative 1e-12 fp64, 1e-5 fp32: BASELINE's tolerances)."""
+1-3 workers; the batched bf16 variant (lsqp4: a ragged last block, a wave with one
+32-column strip, 32 and 2048 columns); every reply against a host fp64 gradient of the
+device's own inputs (relative 1e-12 fp64, 1e-5 fp32 / bf16-in-fp32: BASELINE's tolerances)."""
 import os
 import subprocess
 
@@ -29,7 +30,7 @@ def test_c_client_of_the_abi(built):
     print(out.stdout)
     assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-2000:])
     lines = [ln.split() for ln in out.stdout.splitlines() if ln.startswith("case ")]
-    assert len(lines) == 7 and out.stdout.rstrip().endswith("ok")
+    assert len(lines) == 10 and out.stdout.rstrip().endswith("ok")
     for ln in lines:
         dtype, err = ln[1], float(ln[6])
         assert err <= (1e-12 if dtype == "f64" else 1e-5), ln
