@@ -37,8 +37,16 @@ __device__ __forceinline__ void publish_done(unsigned long long* flag, unsigned 
 // A pre-armed launch its server cancelled: the server's host-pinned cancel word holds the
 // task's seq (set before the doorbell wait is released, cleared once the stream has
 // drained, so every workgroup of the task reads the same value): return before any work.
+// ONE lane per wave reads the word (a host-memory read over the bus) and broadcasts it:
+// with every lane reading, a 192-workgroup task spent ~125 us in these reads (one-GPU
+// N = 2 rehearsal, profiles/r02_arm_go_word.txt).  Call with every lane of the wave active.
 __device__ __forceinline__ bool disarmed(const unsigned long long* go, unsigned long long seq) {
-  return go && __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
+  if (!go) return false;  // kernel argument: wave-uniform
+  unsigned long long v = 0;
+  if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0u)
+    v = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(v)), hi = __builtin_amdgcn_readfirstlane(unsigned(v >> 32));
+  return ((unsigned long long)hi << 32 | lo) == seq;
 }
 
 }  // namespace dev

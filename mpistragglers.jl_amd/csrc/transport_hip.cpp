@@ -330,8 +330,9 @@ class HipComm final : public Comm {
     rt_hz_ = khz > 0 ? double(khz) * 1e3 : 100e6;
     const char* t = std::getenv("MPA_WAIT_TIMEOUT_S");
     timeout_s_ = t ? std::atof(t) : 600.0;
-    const char* arm = std::getenv("MPA_ARM");  // unset: auto (armable(); 0 never, 1 always)
-    arm_mode_ = arm && *arm == '0' ? 0 : arm && *arm == '1' ? 1 : 2;
+    // unset / 0: never pre-arm; 1: arm every eligible worker; 2: when a process serves one
+    const char* arm = std::getenv("MPA_ARM");
+    arm_mode_ = arm && *arm == '1' ? 1 : arm && *arm == '2' ? 2 : 0;
     const char* cb = std::getenv("MPA_COORD_BATCH");
     coord_batches_ = !(cb && *cb == '0');
     fused_tail_ = !env_off("MPA_TAIL");
@@ -701,10 +702,14 @@ class HipComm final : public Comm {
   }
 
   // ---- pre-armed tasks (server) ----
-  // Pre-arming pays where a process serves ONE worker (one worker per GPU, N = 8): with
-  // several, the host-launched path batches them into one launch, which measured faster
-  // than concurrent single-task armed launches (N = 2 rehearsal on one GPU: 1280 vs 1175
-  // it/s, profiles/r01_n2_arm_ab.txt).  MPA_ARM=1 arms every eligible worker, MPA_ARM=0 none.
+  // Off by default (MPA_ARM=2: where a process serves ONE worker; MPA_ARM=1: every eligible
+  // worker).  The armed launch saves the host's doorbell poll + launch (3.2 vs 13.4 us ring ->
+  // start) but its task ran 7-15x longer than the same task launched by the host: every
+  // workgroup reads the host-memory go word before it starts (one-GPU N = 2 rehearsal, c1:
+  // 134 us with every lane reading, 73 us with one lane per wave, 9.6 us host-launched;
+  // 106 vs 48 us per epoch; c2 with 4 armed workers 1.20 vs 0.74 ms; profiles/r02_arm_go_word.txt).
+  // With several workers the host-launched path also batches them into one launch
+  // (profiles/r01_n2_arm_ab.txt).
   bool armable(int64_t rank) const {
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
     if (arm_mode_ == 0 || !((ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty()))
@@ -2127,7 +2132,7 @@ class HipComm final : public Comm {
   bool ahead_update_ = false;
   std::atomic<bool> timing_{false};  // read by the straggler timer thread's launches
   bool debug_ = false;
-  int arm_mode_ = 2;
+  int arm_mode_ = 0;
   // undelayed task batches run on the coordinator stream behind the exchange that delivered
   // their messages (MPA_COORD_BATCH=0: on a launch stream behind a cross-queue event wait,
   // which measured 75-200 us per hand-off on the k-of-n path, profiles/r01_c1_timeline.txt)

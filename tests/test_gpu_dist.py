@@ -44,29 +44,34 @@ def test_lsq_two_processes_hip(built):
     _run(dist_worker.lsq_dist, 2, [0, 1, 1, 1])
 
 
-def test_lsq_two_processes_prearmed(built):
-    """Workers 2-4 on rank 1: 2 and 3 pre-armed (no delays), 4 delayed (host-launched);
-    two serve sessions around a pause."""
+def test_lsq_two_processes_prearmed(built, monkeypatch):
+    """Workers 2-4 on rank 1: 2 and 3 pre-armed (no delays; MPA_ARM=1, pre-arming is
+    opt-in), 4 delayed (host-launched); two serve sessions around a pause."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("MPA_ARM", "1")  # the spawned ranks inherit it
     _run(dist_worker.lsq_dist_armed, 2, [0, 1, 1, 1], [4])
 
 
-def test_lsqb_two_processes_prearmed(built):
+@pytest.mark.parametrize("arm", ["0", "2"])
+def test_lsqb_two_processes(built, monkeypatch, arm):
+    """The batched variant across processes, host-launched (default) and pre-armed."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("MPA_ARM", arm)
     _run(dist_worker.lsqb_dist, 2, [0, 1])
 
 
 @pytest.mark.parametrize("placement,env", [
     ([0, 1, 1, 1], {}),                                   # rank 1 serves 3 workers (host-launched)
-    ([0, 1], {}),                                         # one worker per process: pre-armed
+    ([0, 1], {}),                                         # one worker per process, host-launched
+    ([0, 1], {"MPA_ARM": "2"}),                           # ... pre-armed (opt-in)
     ([0, 1, 1], {"MPA_AHEAD": "0"}),                      # fused epoch kernel, no launch-ahead
     ([0, 1], {"MPA_FUSE": "0"}),                          # the unfused loop
     ([0, 1, 1], {"MPA_XGMI": "0"}),                       # payloads through the host mailbox
-    ([0, 1], {"MPA_XGMI": "0"}),                          # ... pre-armed
+    ([0, 1], {"MPA_XGMI": "0", "MPA_ARM": "2"}),          # ... pre-armed
 ])
 def test_lsq_descent_two_processes(built, placement, env):
     import torch
