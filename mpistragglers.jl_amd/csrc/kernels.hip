@@ -75,6 +75,23 @@ __global__ void __launch_bounds__(kThreads) exchange_kernel(ExchangeArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) wait_words_kernel(WaitWordsArgs a) {
+  const int j = threadIdx.x;
+  bool ok = j >= a.n;
+  const unsigned long long t0 = rt_now();
+  for (unsigned k = 0;; ++k) {
+    if (!ok) ok = __hip_atomic_load(a.word[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= a.target[j];
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;  // every word reached (exit for the whole wave)
+    __builtin_amdgcn_s_sleep(2);
+    if ((k & 63) == 63 && rt_now() - t0 > a.spin_ticks) {  // bounded: report and return
+      if (j == 0) __hip_atomic_fetch_or(a.err, 32u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the replies the remote tasks released
+}
+
+// ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) kmap_task_kernel(KmapArgs a) {
   if (a.kind == MPA_TASK_ECHO) {
     const uint64_t m = a.sl < a.rl ? a.sl : a.rl;
@@ -206,6 +223,12 @@ __global__ void __launch_bounds__(kThreads) read_peak_kernel(const uint4* __rest
 }
 
 }  // namespace
+
+hipError_t launch_wait_words(const WaitWordsArgs& a, hipStream_t s) {
+  if (a.n <= 0 || a.n > kMaxWaitWords) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wait_words_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_exchange(const ExchangeArgs& a, hipStream_t s) {
   int grid = a.block0[a.ncopy];

@@ -31,6 +31,22 @@ struct ExchangeArgs {
 };
 hipError_t launch_exchange(const ExchangeArgs& a, hipStream_t s);
 
+// rank 0's wait for the completion words of the remote workers of a launched-ahead epoch:
+// ONE single-wave launch that polls every word (lane j: word j, system-scope loads of the
+// shared-memory mailbox) until each reaches its target, then acquires at system scope.  It
+// replaces one hipStreamWaitValue64 per remote worker (each a blit kernel of its own, ~4-5 us
+// apiece in series on the coordinator stream: 7 of them per epoch at N = 8).  Bounded:
+// past spin_ticks it sets err bit 32 and returns.
+constexpr int kMaxWaitWords = 64;
+struct WaitWordsArgs {
+  int n;
+  const unsigned long long* word[kMaxWaitWords];
+  unsigned long long target[kMaxWaitWords];
+  unsigned int* err;
+  unsigned long long spin_ticks;
+};
+hipError_t launch_wait_words(const WaitWordsArgs& a, hipStream_t s);
+
 // completion protocol shared by every worker task kernel
 struct Publish {
   unsigned long long* flag;  // host-pinned: seq of the last completed task of the worker

@@ -57,6 +57,9 @@ namespace mpa {
   } while (0)
 
 int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares launch (0 = default)
+// rank 0 waits for remote completions of a launched-ahead epoch with one wait_words_kernel
+// (default) or, MPA_WAIT_VALUE_OPS=1, one hipStreamWaitValue64 per remote worker (round 1)
+const bool g_wait_value_ops = [] { const char* e = std::getenv("MPA_WAIT_VALUE_OPS"); return e && *e == '1'; }();
 
 namespace {
 
@@ -980,12 +983,27 @@ class HipComm final : public Comm {
     // the replies of this call's remote tasks must have landed before the epoch kernel
     // reads them (local tasks are stream-ordered before it on the coordinator stream)
     std::vector<Harvest> hv;
+    WaitWordsArgs ww{};
+    ww.err = err_dev_;
+    ww.spin_ticks = spin_ticks();
     for (const auto& cp : call_posts_) {
       HipWorker& w = w_[size_t(cp.rank - 1)];
-      if (w.remote)
-        HIPCHECK(hipStreamWaitValue64(coord_, region_->dev(&w.box->done), w.seq, hipStreamWaitValueGte, ~0ull));
+      if (w.remote) {
+        if (g_wait_value_ops) {
+          HIPCHECK(hipStreamWaitValue64(coord_, region_->dev(&w.box->done), w.seq, hipStreamWaitValueGte, ~0ull));
+        } else {
+          if (ww.n == kMaxWaitWords) {
+            HIPCHECK(launch_wait_words(ww, coord_));
+            ww.n = 0;
+          }
+          ww.word[ww.n] = region_->dev(&w.box->done);
+          ww.target[ww.n] = w.seq;
+          ++ww.n;
+        }
+      }
       hv.push_back({cp.slot, cp.rank});
     }
+    if (ww.n) HIPCHECK(launch_wait_words(ww, coord_));
     for (int64_t rank : posted) w_[size_t(rank - 1)].seq += 1;  // the ahead epoch's task numbers
     if (tail_pending_) tail_pending_ = false;  // this step ran in the previous launch's tail
     else emit_epoch(hv, hv.size(), posted, u, coord_);
