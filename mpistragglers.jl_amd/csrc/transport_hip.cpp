@@ -348,6 +348,7 @@ class HipComm final : public Comm {
       lsqc_la_ = la && *la == '1' ? 1 : 2;
     }
     hold_ok_ = !env_off("MPA_HOLD");
+    batch_gather_ = !env_off("MPA_GATHER");
     if (const char* e = std::getenv("MPA_LSQP_PF")) lsqp_pfd_ = std::max(0, std::min(8, std::atoi(e)));
     const char* dbg = std::getenv("MPA_DEBUG");
     debug_ = dbg && *dbg == '1';
@@ -695,6 +696,32 @@ class HipComm final : public Comm {
         fresh.push_back(r);
       }
       if (!fresh.empty()) {
+        // rank 0's exchange kernel rings a flush's doorbells one after another: a scan that
+        // caught the first ones looks again for ~2 us before launching, so the flush's tasks
+        // here go out as one batch (the c2 N = 2 trace showed them split over two launches)
+        if (batch_gather_) {
+          const auto g0 = Clock::now();
+          while (std::chrono::duration<double, std::micro>(Clock::now() - g0).count() < 2.0) {
+            for (int64_t r = 1; r <= nworkers_; ++r) {
+              HipWorker& w = w_[size_t(r - 1)];
+              if (!w.here || !w.path_known || w.armed || std::find(fresh.begin(), fresh.end(), r) != fresh.end()) continue;
+              const unsigned long long db = __atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE);
+              if (db != w.seq + 1 || __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) != w.seq) continue;
+              w.seq = db;
+              w.sl = size_t(w.box->msg_bytes);
+              w.rl = size_t(w.box->reply_bytes);
+              check_task(r, tasks_[size_t(r - 1)], w.sl, w.rl);
+              w.x = w.xslot;
+              w.out = reply_dst(w);
+              fresh.push_back(r);
+            }
+            int idle = 0;
+            for (int64_t r = 1; r <= nworkers_; ++r) idle += w_[size_t(r - 1)].here && w_[size_t(r - 1)].path_known;
+            if (int(fresh.size()) >= idle) break;  // every worker served here is posted
+            __builtin_ia32_pause();
+          }
+          std::sort(fresh.begin(), fresh.end());
+        }
         if (timing_) reap_timing(false);
         launch_tasks(fresh, /*staged=*/true);
       } else if (!progress) {
@@ -2151,6 +2178,7 @@ class HipComm final : public Comm {
   std::atomic<bool> timing_{false};  // read by the straggler timer thread's launches
   bool debug_ = false;
   int arm_mode_ = 0;
+  bool batch_gather_ = true;  // MPA_GATHER=0: a server launches whatever one doorbell scan found
   // undelayed task batches run on the coordinator stream behind the exchange that delivered
   // their messages (MPA_COORD_BATCH=0: on a launch stream behind a cross-queue event wait,
   // which measured 75-200 us per hand-off on the k-of-n path, profiles/r01_c1_timeline.txt)
