@@ -116,14 +116,25 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   using P = Pack<T>;
   constexpr int E = P::E;
   __shared__ P red[VPL * 64];           // workgroup partial (VPL*64*E columns)
-  __shared__ unsigned s_ticket;
+  __shared__ unsigned s_ticket, s_cancel;
 
   // which task of the batch this workgroup serves (wave-uniform scan over <= 16 entries)
   int ti = 0;
   while (ti + 1 < batch.ntasks && int(blockIdx.x) >= batch.block0[ti + 1]) ++ti;
   const LsqTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block0[ti];
-  if (disarmed(a.go, a.seq)) return;  // every workgroup of the task alike
+  // A pre-armed task its server cancelled (the host-memory go word holds its seq) computes
+  // but neither writes its reply nor publishes.  The word is read ONCE, by the workgroup that
+  // writes the reply, at that point: every lane of every workgroup reading it before any work
+  // cost a 192-workgroup task ~125 us (profiles/r02_arm_go_word.txt).  Call with the whole
+  // workgroup.
+  auto cancelled = [&]() -> bool {
+    if (!a.go) return false;
+    if (threadIdx.x == 0)
+      s_cancel = __hip_atomic_load(a.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == a.seq;
+    __syncthreads();
+    return s_cancel != 0;
+  };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -220,8 +231,11 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     for (int e = 0; e < E; ++e)
       if (c0 + e < a.cols) out[c0 + e] = s.v[e];
   };
+  bool cx = false;  // cancelled (read by the reply's writer only)
   if (G == 1) {
-    for (int j = tid; j < S; j += kThreads) store_out(j, red[j]);
+    cx = cancelled();
+    if (!cx)
+      for (int j = tid; j < S; j += kThreads) store_out(j, red[j]);
   } else {
     constexpr bool FENCE = (MODE & M_TREE_FENCE) != 0;
     auto put = [&](P* d, const P& v) {
@@ -259,6 +273,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       __syncthreads();
       if (!s_ticket) return;  // an earlier arriver of the group: the last one carries it
       const unsigned next = (count + F - 1) / F;
+      if (next == 1) cx = cancelled();
       const P* src = slab + size_t(first) * stride * S;
       for (int j = tid; j < S; j += kThreads) {
         P t[F];
@@ -271,8 +286,11 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
           if (m < gsize)
 #pragma unroll
             for (int e = 0; e < E; ++e) s.v[e] += t[m].v[e];
-        if (next == 1) store_out(j, s);
-        else put(&slab[size_t(first) * stride * S + j], s);
+        if (next == 1) {
+          if (!cx) store_out(j, s);
+        } else {
+          put(&slab[size_t(first) * stride * S + j], s);
+        }
       }
       if (next == 1) break;
       idx /= F;
@@ -284,6 +302,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   }
   drain_vm();
   __syncthreads();
+  if (cx) return;
   if (tid == 0) publish_done(a.flag, a.seq);
   if (!batch.tail) return;
   // Fused tail: this workgroup finished its task (and published it); the last task of the

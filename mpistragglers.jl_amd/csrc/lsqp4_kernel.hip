@@ -146,7 +146,9 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   int ti = 0;
   while (ti + 1 < batch.ntasks && pidx >= batch.grp0[ti + 1]) ++ti;
   const LsqpTask& a = batch.t[ti];
-  if (disarmed(a.go, a.seq)) return;  // every workgroup of the task alike
+  // a pre-armed task its server cancelled computes but neither writes G nor publishes: the
+  // go word (host memory) is read once per writing wave at the end (disarmed() below), not by
+  // every workgroup before any work (profiles/r02_arm_go_word.txt)
   const int q = pidx - batch.grp0[ti];
   const int ng = batch.grp0[ti + 1] - batch.grp0[ti];
 
@@ -457,11 +459,14 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     if (ct < nct && col < cols)
       *reinterpret_cast<f32x4*>(out + size_t(col) * K + PH * h + 16 * t + 4 * g) = v;
   };
+  bool cx = false;
   if (ng == 1) {
+    cx = disarmed(a.go, a.seq);
+    if (!cx)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) store_out(t, ct, G[t][ct]);
+        for (int ct = 0; ct < NCT; ++ct) store_out(t, ct, G[t][ct]);
   } else {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -482,14 +487,18 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       old = __shfl(old, 0, 64);
       if (old + 1 != gsize) return;  // an earlier arriver of the group: the last one carries it
       const unsigned next = (count + PF - 1) / PF;
+      if (next == 1) cx = disarmed(a.go, a.seq);
       const f32x4* src = slab + size_t(first) * stride * qstride;
 #pragma unroll 4
       for (int j2 = 0; j2 < 2 * NCT; ++j2) {
         const int j = j2 * 64 + lane;
         f32x4 s = ld_wt(src + j);
         for (unsigned m = 1; m < gsize; ++m) s += ld_wt(src + size_t(m) * stride * qstride + j);
-        if (next == 1) store_out(j2 / NCT, j2 % NCT, s);
-        else st_wt(slab + size_t(first) * stride * qstride + j, s);
+        if (next == 1) {
+          if (!cx) store_out(j2 / NCT, j2 % NCT, s);
+        } else {
+          st_wt(slab + size_t(first) * stride * qstride + j, s);
+        }
       }
       if (next == 1) break;
       idx /= PF;
@@ -508,7 +517,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
                                                 __HIP_MEMORY_SCOPE_AGENT);
     if (old + 1 == unsigned(2 * QW)) {
       __hip_atomic_store(&a.ctr[2 * 8 * kLsqpCtrPerSlice], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      publish_done(a.flag, a.seq);
+      if (!cx) publish_done(a.flag, a.seq);  // every slice read the same go word
     }
   }
 }
