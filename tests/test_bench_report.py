@@ -102,3 +102,27 @@ def test_gen_shards_empty_worker_list():
         placement = [(w * world) // 3 for w in range(3)]
         empty = [r for r in range(world) if r not in placement]
         assert empty  # such ranks exist and must not crash
+
+
+def test_trace_window_skips_launches_after_the_timed_region(tmp_path):
+    """tools/trace_window.py averages the `launches` dispatches of the timed region: the ones
+    before the bench's `launches_after_timed` (c5: waitall releases a held 1-task re-dispatch
+    after the timed region; taking the last `launches` dispatches included it)."""
+    import json
+    import subprocess
+    durations = [9.0, 8.5, 8.4, 8.4, 8.6, 1.2]  # warm-up, 4 timed, then the released 1-task launch
+    with open(tmp_path / "trace.csv", "w") as f:
+        f.write("Kernel_Name,Start_Timestamp,End_Timestamp\n")
+        t = 0
+        for d in durations:
+            f.write('"mpa::lsqp4_kernel(mpa::LsqpBatch)",%d,%d\n' % (t, t + int(d * 1e6)))
+            t += int(d * 1e6) + 1000
+    line = {"steps": 4, "roofline": {"launches": 4, "avg_launch_ms": 8.475}, "launches_after_timed": 1}
+    (tmp_path / "bench.log").write_text("progress\n" + json.dumps(line) + "\n")
+    out = tmp_path / "w.json"
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "trace_window.py"), "--trace",
+                           str(tmp_path / "trace.csv"), "--bench-log", str(tmp_path / "bench.log"), "--kernel",
+                           "lsqp4_kernel", "--out", str(out)])
+    w = json.loads(out.read_text())
+    assert w["launches"] == 4 and w["launches_after_timed"] == 1
+    assert abs(w["avg_ms"] - (8.5 + 8.4 + 8.4 + 8.6) / 4) < 1e-9
