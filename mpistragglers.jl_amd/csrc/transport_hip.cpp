@@ -715,9 +715,14 @@ class HipComm final : public Comm {
               w.out = reply_dst(w);
               fresh.push_back(r);
             }
-            int idle = 0;
-            for (int64_t r = 1; r <= nworkers_; ++r) idle += w_[size_t(r - 1)].here && w_[size_t(r - 1)].path_known;
-            if (int(fresh.size()) >= idle) break;  // every worker served here is posted
+            int postable = 0;  // workers here that could still be posted (not busy, not armed)
+            for (int64_t r = 1; r <= nworkers_; ++r) {
+              const HipWorker& w = w_[size_t(r - 1)];
+              postable += w.here && w.path_known && !w.armed &&
+                          (std::find(fresh.begin(), fresh.end(), r) != fresh.end() ||
+                           __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) == w.seq);
+            }
+            if (int(fresh.size()) >= postable) break;  // every worker that could be posted is
             __builtin_ia32_pause();
           }
           std::sort(fresh.begin(), fresh.end());
