@@ -1,6 +1,6 @@
 # Round 2 session 3, final tree (after the go-word change): smoke, full GPU suite, c2 bench
 set -u
-O=gpurun_out/r02end2
+O=${O:-gpurun_out/r02end2}
 mkdir -p $O
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
 tail -2 $O/smoke.log
