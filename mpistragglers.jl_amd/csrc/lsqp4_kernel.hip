@@ -70,10 +70,10 @@ constexpr int SLICE = PRB * ROWB;     // 16 KiB
 constexpr int XS = PH * 2 + 16;       // X staging row stride (bytes)
 constexpr int PF = 4;                 // G tree fan-in
 #ifndef MPA_LSQP4_P2L
-#define MPA_LSQP4_P2L 2               // phase-2 transposed-read chunks in flight ahead
+#define MPA_LSQP4_P2L 1               // phase-2 transposed-read chunks in flight ahead (1 vs 2: -1 %, r02_c5_strip_ring.txt)
 #endif
 #ifndef MPA_LSQP4_AD
-#define MPA_LSQP4_AD 4                // phase-1 fragment read-ahead in k-steps
+#define MPA_LSQP4_AD 3                // phase-1 fragment read-ahead in k-steps (3 beats 2, 4, 6)
 #endif
 static_assert(QW * QKW == kLsqpMaxCols, "4 waves x 512 columns");
 static_assert(NKS == 16 && NCT == 32, "8 strips of 64 columns per wave");
