@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define MPA_ABI_VERSION 2
+#define MPA_ABI_VERSION 3
 
 typedef struct mpa_pool mpa_pool;
 typedef struct mpa_comm mpa_comm;
@@ -90,6 +90,11 @@ enum mpa_task {
   MPA_TASK_LSQ = 4,        /* reply = A_i^T (A_i x - b_i)      (BASELINE workload) */
   MPA_TASK_LSQ_BATCH = 5,  /* reply = A_i^T (A_i X - B_i), X cols x k (bf16 MFMA) */
 };
+
+/* observation points of the state machine, the step kinds of a gated replay
+ * (mpa_comm_set_gate): before phase 1 of asyncmap! (src/MPIAsyncPools.jl:91), before each
+ * MPI.Waitany! with a live request (:161), before MPI.Waitall! (:212) */
+enum mpa_gate_step { MPA_GATE_CALL = 0, MPA_GATE_WAIT = 1, MPA_GATE_WAITALL = 2 };
 
 /* nwait::Function — nwait(epoch, repochs)::Bool (src/MPIAsyncPools.jl:153).
  * Return 1 (true), 0 (false) or a negative value if the callback raised. */
@@ -145,8 +150,11 @@ int mpa_waitall(mpa_pool* pool,
                 int64_t** repochs_out);
 
 /* ---- comm: MPI.Comm + the worker programs ------------------------------------------ */
-/* nworkers device workers with ranks 1..nworkers (rank 0 is the coordinator).
- * devices[w] (w = rank-1) is the HIP device of worker w; NULL = the current device. */
+/* nworkers device workers with ranks 1..nworkers (rank 0 is the coordinator), all on the
+ * calling thread's current HIP device.  devices[w] (w = rank-1) may be given to assert
+ * that: a process serves the workers of its own device only, so any other entry is an
+ * ArgumentError; workers of other GPUs are served by their own processes
+ * (mpa_comm_create_dist, one process per GPU).  NULL = the current device. */
 int mpa_comm_create(int transport, int64_t nworkers, const int* devices, mpa_comm** out);
 void mpa_comm_destroy(mpa_comm* comm);
 int64_t mpa_comm_size(const mpa_comm* comm); /* nworkers + 1, as MPI.Comm_size */
@@ -172,6 +180,24 @@ int mpa_comm_set_delays(mpa_comm* comm, int64_t rank, const int64_t* delays_ns, 
 int64_t mpa_comm_tasks_done(mpa_comm* comm, int64_t rank);
 /* control channel: wait for every outstanding task, then refuse further posts */
 int mpa_comm_shutdown(mpa_comm* comm);
+/* gated replay (a test mode; HIP and HOST transports, rank 0): fixes the order in which
+ * completions become visible to MPI.Test! / Waitany! / Waitall! (src/MPIAsyncPools.jl:99,
+ * 161,212).  Step k (kinds[k] = MPA_GATE_*) is taken at the k-th observation point of the
+ * state machine and releases one more completion of each worker rank in
+ * ranks[offsets[k] .. offsets[k+1]); a request reads as complete once its task has
+ * finished and been released, and the step waits until every task it releases has
+ * finished.  A step of the wrong kind is an error; after the last step the next
+ * observation switches the gate off; nsteps == 0 switches it off now.  Schedules come from
+ * the oracle's virtual clock (oracle/oracle.py gate_schedule), so the device replays the
+ * oracle's trace bit for bit whatever the physical completion order. */
+int mpa_comm_set_gate(mpa_comm* comm, int64_t nsteps, const int* kinds, const int64_t* offsets,
+                      const int64_t* ranks);
+/* event counters (tests, diagnostics); -1 for a name the transport does not count.  HIP
+ * rank 0: "held" stale re-dispatches whose launch was held (src/MPIAsyncPools.jl:177-184,
+ * DESIGN.md §5), "held_joined" of them launched inside a later batch, "held_alone" launched
+ * on their own (a wait that would block, a gated release, waitall!, shutdown);
+ * "gate_steps" gated-replay steps taken. */
+int64_t mpa_comm_counter(mpa_comm* comm, const char* name);
 /* ---- multi-process communicators: one process per GPU ------- */
 /* placement[w] = the process rank that serves worker w+1 (rank 0 is the coordinator's own
  * process).  my_rank 0 creates the shared-memory mailboxes `shm_name` (POSIX shm name,

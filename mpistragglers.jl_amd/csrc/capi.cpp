@@ -308,6 +308,19 @@ int mpa_comm_shutdown(mpa_comm* comm) {
   return guarded([&] { comm_of(comm).shutdown(); });
 }
 
+int mpa_comm_set_gate(mpa_comm* comm, int64_t nsteps, const int* kinds, const int64_t* offsets, const int64_t* ranks) {
+  return guarded([&] { comm_of(comm).set_gate(kinds, offsets, ranks, nsteps); });
+}
+
+int64_t mpa_comm_counter(mpa_comm* comm, const char* name) {
+  int64_t r = -1;
+  const int rc = guarded([&] {
+    if (!name) mpa::fail(MPA_ARGUMENT_ERROR, "name is NULL");
+    r = comm_of(comm).counter(name);
+  });
+  return rc == MPA_OK ? r : -1;
+}
+
 int mpa_comm_set_timing(mpa_comm* comm, int enable) {
   return guarded([&] {
     mpa::Comm& c = comm_of(comm);

@@ -77,10 +77,45 @@ class Comm {
   virtual void shutdown() = 0;
   bool is_shutdown() const { return shutdown_; }
 
+  // ---- gated replay (mpa_comm_set_gate, gate.cpp) ----
+  // A test mode that fixes the completion order to a schedule.  The state machine calls
+  // gate() at each of its observation points (pool.cpp: before phase 1 of asyncmap!,
+  // before each Waitany! with a live request, before Waitall!); step k of the schedule
+  // names the workers that release one more completion there.  A worker's request then
+  // reads as complete only once its task has finished AND been released, and gate() waits
+  // until every task it releases has finished, so each Test!/Waitany! sees exactly the set
+  // of completions the schedule says (the oracle's virtual-clock set, ties included).
+  // After the last step the next observation switches the gate off.
+  void set_gate(const int* kinds, const int64_t* offsets, const int64_t* ranks, int64_t nsteps);
+  void gate(int kind);
+  bool gated() const { return gate_on_; }
+  size_t gate_steps_taken() const { return gate_step_; }
+
+  // event counters of the transport for tests and diagnostics (mpa_comm_counter); -1 for a
+  // name the transport does not count
+  virtual int64_t counter(const char* name) const { (void)name; return -1; }
+
  protected:
+  bool gate_open(int64_t rank, uint64_t seq) const { return !gate_on_ || gate_rel_[size_t(rank - 1)] >= seq; }
+  void gate_off() { gate_on_ = false; }
+  // transport hooks of the gate: tasks posted to / finished by a worker, make sure a posted
+  // task is launched (the HIP transport's held re-dispatches), check errors while waiting
+  virtual bool gate_supported() const { return false; }
+  virtual uint64_t gate_posted(int64_t rank) { (void)rank; return 0; }
+  virtual uint64_t gate_finished(int64_t rank) { (void)rank; return 0; }
+  virtual void gate_launch(int64_t rank) { (void)rank; }
+  virtual void gate_poll(double waited_s) { (void)waited_s; }
+
   int64_t nworkers_;
   std::vector<TaskSpec> tasks_;
   bool shutdown_ = false;
+
+ private:
+  bool gate_on_ = false;
+  size_t gate_step_ = 0;
+  std::vector<int> gate_kinds_;
+  std::vector<int64_t> gate_off_, gate_ranks_;
+  std::vector<uint64_t> gate_rel_;  // completions released per worker
 };
 
 Comm* make_sim_comm(int64_t nworkers);

@@ -80,6 +80,7 @@ void asyncmap(Pool& p, const AsyncmapArgs& a) {
   c.begin_call(b);
 
   p.epoch = a.epoch;                                                               // :87
+  c.gate(MPA_GATE_CALL);  // gated replay: the completions phase 1's Test! may see (gate.cpp)
 
   for (int64_t i = 0; i < comm_size; ++i) {                                        // :91-114
     const size_t k = size_t(i);
@@ -118,6 +119,11 @@ void asyncmap(Pool& p, const AsyncmapArgs& a) {
            a.nwait_typename ? a.nwait_typename : "?");
     }
     c.set_wait_hold(a.nwait_kind == MPA_NWAIT_INT && nowed >= a.nwait - nrecv);
+    if (c.gated()) {  // the completions this Waitany! may see (a call that finds none live is MPI_UNDEFINED)
+      bool live = false;
+      for (int64_t j = 0; j < comm_size; ++j) live |= p.rreq_live[size_t(j)] != 0;
+      if (live) c.gate(MPA_GATE_WAIT);
+    }
     const int64_t i = c.waitany(comm_size, p.ranks.data(), p.rreq_live.data());   // :161
     if (i < 0) {  // MPI_UNDEFINED: undefined in the reference; an error here
       c.end_call();
@@ -160,6 +166,7 @@ void waitall(Pool& p, void* recvbuf, size_t recv_bytes, size_t recv_length, void
   b.rl = irecv_bytes / size_t(comm_size);
   b.n = comm_size;
   c.begin_call(b);
+  c.gate(MPA_GATE_WAITALL);
   c.waitall(comm_size, p.ranks.data(), p.rreq_live.data());                        // :212
   for (int64_t i = 0; i < comm_size; ++i) {                                        // :213-221
     const size_t k = size_t(i);

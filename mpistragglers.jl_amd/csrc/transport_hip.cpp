@@ -551,6 +551,7 @@ class HipComm final : public Comm {
     if (held_.empty()) return;
     std::vector<int64_t> h;
     h.swap(held_);
+    n_held_alone_ += int64_t(h.size());
     launch_tasks(h, /*staged=*/false);
   }
 
@@ -607,6 +608,7 @@ class HipComm final : public Comm {
   }
 
   void shutdown() override {
+    gate_off();
     release_held();
     if (role_ != SERVER) {
       const auto t0 = Clock::now();
@@ -859,11 +861,15 @@ class HipComm final : public Comm {
       if (w_[size_t(rank - 1)].remote) continue;
       const TaskSpec& ts = tasks_[size_t(rank - 1)];
       if (hold_next_ && (ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty())
+      {
         held_.push_back(rank);  // flush_stale(): joins the next batch
+        ++n_held_;
+      }
       else
         here.push_back(rank);
     }
     if (!here.empty() && !held_.empty() && !hold_next_) {  // held re-dispatches join this batch
+      n_held_joined_ += int64_t(held_.size());
       here.insert(here.begin(), held_.begin(), held_.end());
       held_.clear();
     }
@@ -1162,7 +1168,30 @@ class HipComm final : public Comm {
 
   bool done(int64_t rank) const {
     const HipWorker& w = w_[size_t(rank - 1)];
-    return __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) >= w.seq;
+    return __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) >= w.seq && gate_open(rank, w.seq);
+  }
+
+  int64_t counter(const char* name) const override {
+    const std::string k = name;
+    if (k == "held") return n_held_;
+    if (k == "held_joined") return n_held_joined_;
+    if (k == "held_alone") return n_held_alone_;
+    if (k == "gate_steps") return int64_t(gate_steps_taken());
+    return -1;
+  }
+
+  // gated replay hooks (gate.cpp): the coordinator's view of its workers
+  bool gate_supported() const override { return role_ != SERVER; }
+  uint64_t gate_posted(int64_t rank) override { return w_[size_t(rank - 1)].seq; }
+  uint64_t gate_finished(int64_t rank) override { return __atomic_load_n(w_[size_t(rank - 1)].flag_host, __ATOMIC_ACQUIRE); }
+  void gate_launch(int64_t rank) override {
+    // a held re-dispatch the schedule completes: launch it (with the rest of the held batch)
+    if (std::find(held_.begin(), held_.end(), rank) != held_.end()) release_held();
+  }
+  void gate_poll(double waited_s) override {
+    watchdog(Clock::now(), /*timeout=*/false);
+    if (timeout_s_ > 0 && waited_s > timeout_s_)
+      fail(MPA_DEVICE_ERROR, "gated replay: waited more than %.0f s for a released task (MPA_WAIT_TIMEOUT_S)", timeout_s_);
   }
 
   unsigned device_error() const {
@@ -2155,6 +2184,8 @@ class HipComm final : public Comm {
   bool hold_next_ = false;  // set while flush_stale() flushes
   bool may_hold_ = false;   // this call's wait completes without the held tasks (set_wait_hold)
   std::vector<int64_t> held_;  // held re-dispatches, launched with the next batch
+  // held re-dispatches: held, later joined a batched launch, launched on their own
+  int64_t n_held_ = 0, n_held_joined_ = 0, n_held_alone_ = 0;
   bool lsqp8_ = false;  // MPA_LSQP=8: the eight-wave single pass (lsqp_kernel.hip)
   bool lsqc_ = false;   // MPA_LSQP=c: the column-pair single pass (lsqc_kernel.hip)
   int lsqc_la_ = 2;     // MPA_LSQC_LA: its phase-1 lookahead in blocks (2; 1 for A/B)

@@ -141,6 +141,7 @@ class HostDistComm final : public Comm {
   int64_t tasks_done(int64_t rank) override { return int64_t(done_word(rank)); }
 
   void shutdown() override {
+    gate_off();
     if (my_rank_ == 0) {
       for (int64_t r = 1; r <= nworkers_; ++r)
         while (!done(r)) std::this_thread::yield();
@@ -204,7 +205,18 @@ class HostDistComm final : public Comm {
     return w.remote || my_rank_ != 0 ? __atomic_load_n(&w.box->done, __ATOMIC_ACQUIRE)
                                      : __atomic_load_n(&w.local_done, __ATOMIC_ACQUIRE);
   }
-  bool done(int64_t rank) const { return done_word(rank) >= w_[size_t(rank - 1)].seq; }
+  bool done(int64_t rank) const {
+    const unsigned long long seq = w_[size_t(rank - 1)].seq;
+    return done_word(rank) >= seq && gate_open(rank, seq);
+  }
+
+  // gated replay hooks (gate.cpp)
+  bool gate_supported() const override { return my_rank_ == 0; }
+  uint64_t gate_posted(int64_t rank) override { return w_[size_t(rank - 1)].seq; }
+  uint64_t gate_finished(int64_t rank) override { return done_word(rank); }
+  void gate_poll(double waited_s) override {
+    if (waited_s > 600) fail(MPA_ERROR, "gated replay: waited more than 600 s for a released task");
+  }
 
   std::vector<HostWorker> w_;
   ShmRegion* region_;

@@ -16,6 +16,7 @@ MPA_OK, MPA_ARGUMENT_ERROR, MPA_DIMENSION_MISMATCH, MPA_ERROR, MPA_DEVICE_ERROR,
 MPA_F32, MPA_F64, MPA_BF16 = 0, 1, 2
 MPA_TRANSPORT_HIP, MPA_TRANSPORT_SIM, MPA_TRANSPORT_HOST = 0, 1, 2
 MPA_NWAIT_INT, MPA_NWAIT_FN, MPA_NWAIT_OTHER = 0, 1, 2
+MPA_GATE_CALL, MPA_GATE_WAIT, MPA_GATE_WAITALL = 0, 1, 2
 (MPA_TASK_NONE, MPA_TASK_ECHO, MPA_TASK_KMAP1, MPA_TASK_KMAP2, MPA_TASK_LSQ,
  MPA_TASK_LSQ_BATCH) = range(6)
 

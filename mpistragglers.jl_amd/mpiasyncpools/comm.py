@@ -88,6 +88,26 @@ class _Comm:
         """Control channel (examples/iterative_example.jl:49-52): drain, then stop."""
         check(lib().mpa_comm_shutdown(self._h))
 
+    def counter(self, name):
+        """An event counter of the transport (mpa_comm_counter): "held", "held_joined",
+        "held_alone", "gate_steps"; -1 if the transport does not count it."""
+        return int(lib().mpa_comm_counter(self._h, name.encode()))
+
+    def set_gate(self, kinds, offsets, ranks):
+        """Gated replay (mpa_comm_set_gate, a test mode): at the k-th observation point of
+        the state machine (kinds[k]: MPA_GATE_CALL / _WAIT / _WAITALL) one more completion of
+        each rank in ranks[offsets[k]:offsets[k+1]] becomes visible, and only released
+        completions are.  The schedule comes from the oracle (OracleSim.gate_schedule);
+        kinds == [] switches the gate off."""
+        k = np.ascontiguousarray(kinds, dtype=np.int32)
+        o = np.ascontiguousarray(offsets, dtype=np.int64)
+        r = np.ascontiguousarray(ranks, dtype=np.int64)
+        if k.size and o.size != k.size + 1:
+            raise ArgumentError("gate schedule: offsets needs one entry more than kinds")
+        self._keep["gate"] = (k, o, r)
+        check(lib().mpa_comm_set_gate(self._h, int(k.size), k.ctypes.data if k.size else None,
+                                      o.ctypes.data if o.size else None, r.ctypes.data if r.size else None))
+
     def _before_call(self, sendbuf):
         pass
 

@@ -98,6 +98,7 @@ int orc_asyncmap(orc_pool* p, const orc_transport* tp,
   const size_t rl = irecv_bytes / (size_t)comm_size;                        /* :81 */
 
   p->epoch = epoch;                                                         /* :87 */
+  if (tp->observe) tp->observe(tp->ctx, ORC_OBS_CALL);
 
   /* phase 1: harvest results received since the last call :91-114 */
   for (int64_t i = 0; i < comm_size; ++i) {
@@ -198,7 +199,18 @@ struct orc_sim {
   uint8_t* delivered;
   orc_event* ev;
   int64_t nev, capev;
+  orc_obs* obs;
+  int64_t nobs, capobs;
 };
+
+static void sim_log(orc_sim* s, int64_t kind, int64_t worker, int64_t t, int64_t done) {
+  if (s->nobs == s->capobs) {
+    s->capobs = s->capobs ? 2 * s->capobs : 1024;
+    s->obs = (orc_obs*)realloc(s->obs, (size_t)s->capobs * sizeof(orc_obs));
+  }
+  orc_obs o = {kind, worker, t, done, s->now};
+  s->obs[s->nobs++] = o;
+}
 
 orc_sim* orc_sim_create(int64_t nworkers, int kind, const int64_t* durations_ns, int64_t ncols,
                         int64_t compute_ns) {
@@ -229,6 +241,7 @@ void orc_sim_destroy(orc_sim* s) {
   for (int64_t i = 0; i < s->nworkers; ++i) free(s->snap[i]);
   free(s->durations); free(s->t); free(s->post_ns); free(s->done_ns); free(s->rank);
   free(s->rbuf); free(s->rl); free(s->snap); free(s->sl); free(s->delivered); free(s->ev);
+  free(s->obs);
   free(s);
 }
 
@@ -246,6 +259,7 @@ static void sim_post(void* ctx, int64_t i, int64_t rank, const uint8_t* sbuf, si
   s->post_ns[i] = s->now;
   s->done_ns[i] = s->now + s->durations[i * s->ncols + (s->t[i] - 1) % s->ncols] + s->compute_ns;
   s->delivered[i] = 0;
+  sim_log(s, ORC_OBS_POST, i, s->t[i], s->done_ns[i]);
 }
 
 /* the worker's reply lands in irecvbufs[i] (MPI.Isend on the worker side) */
@@ -310,11 +324,12 @@ static int64_t sim_waitany(void* ctx, int64_t n, const uint8_t* live) {
   int64_t best = -1;
   for (int64_t i = 0; i < n; ++i) {
     if (!live[i]) continue;
-    if (s->done_ns[i] <= s->now) { sim_deliver(s, i); return i; }
+    if (s->done_ns[i] <= s->now) { sim_log(s, ORC_OBS_WAIT, -1, 0, 0); sim_deliver(s, i); return i; }
     if (best < 0 || s->done_ns[i] < s->done_ns[best]) best = i;
   }
   if (best < 0) return -1;
   s->now = s->done_ns[best];
+  sim_log(s, ORC_OBS_WAIT, -1, 0, 0);
   sim_deliver(s, best);
   return best;
 }
@@ -325,9 +340,12 @@ static void sim_waitall(void* ctx, int64_t n, const uint8_t* live) {
   for (int64_t i = 0; i < n; ++i)
     if (live[i] && s->done_ns[i] > tmax) tmax = s->done_ns[i];
   s->now = tmax;
+  sim_log(s, ORC_OBS_WAITALL, -1, 0, 0);
   for (int64_t i = 0; i < n; ++i)
     if (live[i]) sim_deliver(s, i);
 }
+
+static void sim_observe(void* ctx, int kind) { sim_log((orc_sim*)ctx, kind, -1, 0, 0); }
 
 static uint64_t sim_time(void* ctx) { return (uint64_t)((orc_sim*)ctx)->now; }
 
@@ -338,11 +356,18 @@ void orc_sim_transport(orc_sim* s, orc_transport* out) {
   out->waitany = sim_waitany;
   out->waitall = sim_waitall;
   out->time_ns = sim_time;
+  out->observe = sim_observe;
 }
 
 void orc_sim_advance(orc_sim* s, int64_t dt_ns) { s->now += dt_ns; }
 int64_t orc_sim_now(const orc_sim* s) { return s->now; }
 int64_t orc_sim_tasks(const orc_sim* s, int64_t worker) { return s->t[worker]; }
+
+int64_t orc_sim_obs(const orc_sim* s, orc_obs* out, int64_t cap) {
+  int64_t m = s->nobs < cap ? s->nobs : cap;
+  if (out && m > 0) memcpy(out, s->obs, (size_t)m * sizeof(orc_obs));
+  return s->nobs;
+}
 
 int64_t orc_sim_events(const orc_sim* s, orc_event* out, int64_t cap) {
   int64_t m = s->nev < cap ? s->nev : cap;

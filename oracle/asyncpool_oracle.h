@@ -54,7 +54,14 @@ typedef struct orc_transport {
   void (*waitall)(void* ctx, int64_t n, const uint8_t* live);
   /* Base.time_ns() */
   uint64_t (*time_ns)(void* ctx);
+  /* optional (NULL = none): the call's observation point before phase 1, ORC_OBS_CALL; the
+   * observation points of Waitany!/Waitall! are the transport's own calls above */
+  void (*observe)(void* ctx, int kind);
 } orc_transport;
+
+/* observation points of the state machine (the step kinds of a gated replay schedule,
+ * include/mpiasyncpools.h MPA_GATE_*), plus the post records of the sim's log */
+enum { ORC_OBS_CALL = 0, ORC_OBS_WAIT = 1, ORC_OBS_WAITALL = 2, ORC_OBS_POST = 3 };
 
 typedef struct orc_pool {
   int64_t n;
@@ -113,6 +120,15 @@ int64_t orc_sim_tasks(const orc_sim* s, int64_t worker);
  * observed by the coordinator */
 typedef struct { int64_t worker, t, post_ns, done_ns, seen_ns; } orc_event;
 int64_t orc_sim_events(const orc_sim* s, orc_event* out, int64_t cap);
+
+/* observation log of the simulated transport, in program order: ORC_OBS_POST for every
+ * task posted (worker, t, done_ns), ORC_OBS_CALL / _WAIT / _WAITALL for every observation
+ * point with the virtual time it observes (now; a Waitany! that blocks logs the time it
+ * advances to, one that finds no live request logs nothing).  The completions an
+ * observation sees are exactly the posted tasks with done_ns <= now: the gate schedule of a
+ * device replay (oracle/oracle.py gate_schedule). */
+typedef struct { int64_t kind, worker, t, done_ns, now; } orc_obs;
+int64_t orc_sim_obs(const orc_sim* s, orc_obs* out, int64_t cap);
 
 #ifdef __cplusplus
 }

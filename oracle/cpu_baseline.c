@@ -161,7 +161,7 @@ int main(int argc, char** argv) {
     while (atomic_load(&w[i].done) != 0) _mm_pause();
 
   shm_transport st = {n, w};
-  orc_transport tp = {&st, t_post, t_test, t_waitany, t_waitall, t_time};
+  orc_transport tp = {&st, t_post, t_test, t_waitany, t_waitall, t_time, NULL};
   orc_pool* pool = orc_pool_create(n, NULL, 0, nwait);
   float* x = (float*)calloc((size_t)cols, sizeof(float));
   float* isend = (float*)calloc((size_t)n * (size_t)cols, sizeof(float));

@@ -135,7 +135,7 @@ int main(int argc, char** argv) {
 
   mpi_ctx m = {n, (MPI_Request*)malloc(sizeof(MPI_Request) * (size_t)n)};
   for (long long i = 0; i < n; ++i) m.rreq[i] = MPI_REQUEST_NULL;
-  orc_transport tp = {&m, t_isend_irecv, t_test, t_waitany, t_waitall, t_time_ns};
+  orc_transport tp = {&m, t_isend_irecv, t_test, t_waitany, t_waitall, t_time_ns, NULL};
   orc_pool* p = orc_pool_create(n, NULL, 0, n);
   double send = 0, *isend = calloc((size_t)n, sizeof(double));
   double *recv = calloc((size_t)(3 * n), sizeof(double)), *irecv = calloc((size_t)(3 * n), sizeof(double));

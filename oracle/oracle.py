@@ -81,13 +81,16 @@ def lib():
         L.orc_sim_tasks.argtypes = [C.c_void_p, C.c_int64]
         L.orc_sim_events.restype = C.c_int64
         L.orc_sim_events.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.orc_sim_obs.restype = C.c_int64
+        L.orc_sim_obs.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         _lib = L
     return _lib
 
 
 class _Transport(C.Structure):
     _fields_ = [("ctx", C.c_void_p), ("isend_irecv", C.c_void_p), ("test", C.c_void_p),
-                ("waitany", C.c_void_p), ("waitall", C.c_void_p), ("time_ns", C.c_void_p)]
+                ("waitany", C.c_void_p), ("waitall", C.c_void_p), ("time_ns", C.c_void_p),
+                ("observe", C.c_void_p)]
 
 
 class _PoolStruct(C.Structure):
@@ -97,6 +100,16 @@ class _PoolStruct(C.Structure):
                 ("stimestamps", C.POINTER(C.c_int64)), ("latency", C.POINTER(C.c_double)),
                 ("rreq_live", C.POINTER(C.c_uint8)),
                 ("nwait", C.c_int64), ("epoch", C.c_int64), ("errmsg", C.c_char * 512)]
+
+
+class _Obs(C.Structure):
+    _fields_ = [("kind", C.c_int64), ("worker", C.c_int64), ("t", C.c_int64), ("done_ns", C.c_int64),
+                ("now", C.c_int64)]
+
+
+# observation kinds of the sim's log (asyncpool_oracle.h ORC_OBS_*; the first three are the
+# step kinds of a gated replay, include/mpiasyncpools.h MPA_GATE_*)
+OBS_CALL, OBS_WAIT, OBS_WAITALL, OBS_POST = 0, 1, 2, 3
 
 
 class _Event(C.Structure):
@@ -172,6 +185,34 @@ class OracleSim:
         buf = (_Event * max(n, 1))()
         lib().orc_sim_events(self._h, buf, n)
         return [(e.worker, e.t, e.post_ns, e.done_ns, e.seen_ns) for e in buf[:n]]
+
+    def observations(self):
+        """The sim's observation log: (kind, worker, t, done_ns, now) in program order."""
+        n = lib().orc_sim_obs(self._h, None, 0)
+        buf = (_Obs * max(n, 1))()
+        lib().orc_sim_obs(self._h, buf, n)
+        return [(o.kind, o.worker, o.t, o.done_ns, o.now) for o in buf[:n]]
+
+    def gate_schedule(self, ranks=None):
+        """The gated-replay schedule of everything run on this sim so far (the arguments
+        of mpa_comm_set_gate): at every observation point, the tasks whose virtual
+        completion time has passed and that no earlier point released -- exactly the
+        completions the oracle's Test!/Waitany!/Waitall! could see there.  `ranks` maps
+        the sim's worker positions (pool positions) to comm ranks (default 1..n).
+
+        Returns (kinds, offsets, ranks) as int32 / int64 / int64 arrays."""
+        ranks = np.arange(1, self.nworkers + 1) if ranks is None else np.asarray(ranks)
+        pending, kinds, offs, rel = [], [], [0], []
+        for kind, w, t, done, now in self.observations():
+            if kind == OBS_POST:
+                pending.append((done, int(ranks[w])))
+                continue
+            rel.extend(sorted(r for d, r in pending if d <= now))
+            pending = [p for p in pending if p[0] > now]
+            kinds.append(kind)
+            offs.append(len(rel))
+        return (np.asarray(kinds, dtype=np.int32), np.asarray(offs, dtype=np.int64),
+                np.asarray(rel, dtype=np.int64))
 
     def __del__(self):
         try:

@@ -1,0 +1,98 @@
+"""Gated replay (mpa_comm_set_gate), shared by the CPU test on the HOST transport
+(tests/test_gate_cpu.py) and the device tests on the HIP transport (tests/test_gpu_gated.py).
+
+The oracle runs a scenario on its virtual clock and logs, at every observation point of
+the state machine (before phase 1 of asyncmap!, each Waitany!, each Waitall!), which task
+completions it could see there (oracle/oracle.py OracleSim.gate_schedule).  The product
+is handed that schedule: a request reads as complete only once its task has finished AND
+the schedule has released it, so every Test!/Waitany!/Waitall! sees the oracle's set of
+completions and the product must reproduce the oracle's trace bit for bit, whatever order
+the tasks really finish in (ties included: released together, Waitany! must take the
+lowest index, src/MPIAsyncPools.jl:161 over MPICH's array scan).
+"""
+import importlib.util
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def make_golden():
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg
+
+
+def scenarios():
+    return json.load(open(os.path.join(GOLDEN, "traces.json")))["scenarios"]
+
+
+def oracle_gate(sc):
+    """(oracle records, gate schedule) of a scenario; the schedule is in comm ranks."""
+    mg = make_golden()
+    out, sim = mg.run_scenario(sc, return_sim=True)
+    n = sc["n"]
+    return out, sim.gate_schedule(sc.get("ranks", list(range(1, n + 1))))
+
+
+def replay(M, sc, comm, buf, host, predicate):
+    """Run a scenario's ops on the product through `comm`; the oracle's record layout.
+    `buf(k)` makes a float64 buffer of k elements, `host(b)` reads one back as numpy."""
+    n = sc["n"]
+    ranks = sc.get("ranks", list(range(1, n + 1)))
+    pool = M.MPIAsyncPool(ranks, epoch0=sc.get("epoch0", 0), nwait=sc.get("default_nwait"))
+    elems, chunk = sc.get("send_elems", 1), sc.get("chunk_elems", 3)
+    send, isend = buf(elems), buf(n * elems)
+    recv, irecv = buf(n * chunk), buf(n * chunk)
+    out = []
+    for op in sc["ops"]:
+        if op["op"] == "waitall":
+            M.waitall_(pool, recv, irecv)
+        else:
+            send[0] = float(op.get("send", 0))
+            nw = op.get("nwait")
+            nw = predicate(nw) if isinstance(nw, str) else nw
+            M.asyncmap_(pool, send, recv, isend, irecv, comm, nwait=nw, epoch=op.get("epoch"), tag=0)
+        out.append({"repochs": pool.repochs.tolist(), "sepochs": pool.sepochs.tolist(),
+                    "active": pool.active.astype(int).tolist(), "epoch": int(pool.epoch),
+                    "latency_s": pool.latency.tolist(), "recv": np.asarray(host(recv)).tolist()})
+    return out, pool
+
+
+KEYS = ("repochs", "sepochs", "active", "epoch", "recv")
+
+
+def mismatches(name, got, ref):
+    """Every (op, field) where the product's trace differs from the oracle's."""
+    bad = []
+    for k, (g, r) in enumerate(zip(got, ref)):
+        for key in KEYS:
+            if g[key] != r[key]:
+                bad.append((name, k, key, g[key], r[key]))
+    if len(got) != len(ref):
+        bad.append((name, "ops", len(got), len(ref)))
+    return bad
+
+
+def random_scenario(seed):
+    """A random pool / schedule / op mix (ties from 0-5 ms durations, nwait integers,
+    counting predicates and test/kmap2.jl:65's predicate, explicit epochs, waitall!s)."""
+    rng = np.random.default_rng(5000 + seed)
+    n = int(rng.integers(1, 10))
+    ops = []
+    for _ in range(int(rng.integers(5, 50))):
+        if rng.random() < 0.08:
+            ops.append({"op": "waitall"})
+            continue
+        op = {"op": "asyncmap", "send": int(rng.integers(0, 1000)),
+              "advance_ns": int(rng.integers(0, 3)) * 1_000_000 if rng.random() < 0.3 else 0}
+        k = rng.random()
+        op["nwait"] = int(rng.integers(0, n + 1)) if k < 0.6 else f"count_{int(rng.integers(0, n + 1))}" if k < 0.8 else "first"
+        if rng.random() < 0.2:
+            op["epoch"] = int(rng.integers(-3, 40))
+        ops.append(op)
+    d = rng.integers(0, 6, size=(n, 8)) * 1_000_000
+    return {"name": f"rand{seed}", "n": n, "worker": "kmap2", "durations_ns": d.ravel().tolist(), "ops": ops}

@@ -61,8 +61,9 @@ def kmap2_ops(epochs=100):
     return ops
 
 
-def run_scenario(sc):
-    """Run a scenario on the oracle; returns the list of per-op records."""
+def run_scenario(sc, return_sim=False):
+    """Run a scenario on the oracle; returns the list of per-op records (and the oracle's
+    sim, whose observation log gives the gated-replay schedule, with return_sim)."""
     n, comm_n = sc["n"], sc.get("comm_workers", sc["n"])
     ranks = sc.get("ranks", list(range(1, n + 1)))
     kind = {"kmap2": O.ORC_WORKER_KMAP2, "tag": O.ORC_WORKER_TAG, "echo": O.ORC_WORKER_ECHO,
@@ -94,7 +95,7 @@ def run_scenario(sc):
                     "latency_ns": [int(round(v * 1e9)) for v in pool.latency],
                     "t_start": int(t0), "t_end": int(sim.now),
                     "recv": recv.view(np.int64).tolist() if sc["worker"] == "tag" else recv.tolist()})
-    return out
+    return (out, sim) if return_sim else out
 
 
 def _events(sc):

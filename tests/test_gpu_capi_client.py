@@ -8,8 +8,12 @@ at vector `lane` of the row instead of vector 0, past the end of A on the last r
 lsq_kernel.hip / lsqw_kernel.hip).  Cases: narrow rows with a partial vector group (fp64 64
 columns, fp32 100 and 8), a full-width narrow row, wide rows with a one-vector last slice;
 1-3 workers; the batched bf16 variant (lsqp4: a ragged last block, a wave with one
-32-column strip, 32 and 2048 columns); every reply against a host fp64 gradient of the
-device's own inputs (relative 1e-12 fp64, 1e-5 fp32 / bf16-in-fp32: BASELINE's tolerances)."""
+32-column strip, 32 and 2048 columns; the two-pass kernels at 2080 and 4096 columns); every
+reply against a host fp64 gradient of the device's own inputs (relative 1e-12 fp64, 1e-5
+fp32 / bf16-in-fp32: BASELINE's tolerances).  Beyond one call: mpa_lsq_descent (fused tail,
+launch-ahead; the epoch kernel for wide rows) and mpa_lsqb_descent for several epochs against
+a host fp64 replay, and a k-of-n run under a gated schedule with a stale harvest in the wait
+loop, its held re-dispatch, a phase-1 harvest, a tie and waitall!."""
 import os
 import subprocess
 
@@ -30,7 +34,7 @@ def test_c_client_of_the_abi(built):
     print(out.stdout)
     assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-2000:])
     lines = [ln.split() for ln in out.stdout.splitlines() if ln.startswith("case ")]
-    assert len(lines) == 10 and out.stdout.rstrip().endswith("ok")
+    assert len(lines) == 19 and out.stdout.rstrip().endswith("ok")
     for ln in lines:
         dtype, err = ln[1], float(ln[6])
         assert err <= (1e-12 if dtype == "f64" else 1e-5), ln

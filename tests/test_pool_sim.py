@@ -75,24 +75,6 @@ def test_product_matches_golden_traces(name):
             assert g[key] == r[key], (name, k, key)
 
 
-@pytest.mark.parametrize("name", [s["name"] for s in GOLD if s["name"].startswith("gpu_sep")])
-def test_scaled_delays_keep_the_trace(name):
-    """tests/test_gpu_configs.py and tests/test_gpu.py run these schedules with every delay
-    doubled (DELAY_SCALE):
-    on the oracle and on the product's SimComm the trace (repochs, sepochs, active, recvbuf)
-    is the golden one, only the clock scales."""
-    import test_gpu_configs as C
-    mg = _load_make_golden()
-    sc = dict(next(s for s in GOLD if s["name"] == name))
-    sc["durations_ns"] = [C.DELAY_SCALE * d for d in sc["durations_ns"]]
-    for got in (mg.run_scenario(sc), run_product(sc, mg.predicate)):
-        for k, (g, r) in enumerate(zip(got, sc["results"])):
-            for key in ("repochs", "sepochs", "active", "epoch", "recv"):
-                assert g[key] == r[key], (name, k, key)
-            assert g["t_end"] == C.DELAY_SCALE * r["t_end"], (name, k)
-            assert g["latency_ns"] == [C.DELAY_SCALE * v for v in r["latency_ns"]], (name, k)
-
-
 @pytest.mark.parametrize("seed", range(12))
 def test_product_matches_oracle_random(seed):
     """Random pools, delays (with ties), nwait kinds, explicit epochs and waitall!s."""
