@@ -57,9 +57,12 @@ namespace mpa {
   } while (0)
 
 int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares launch (0 = default)
+// A/B switches of the measurement build only (make MEASURE=1): the product reads none of
+// them, so the shipped behaviour cannot be switched off by an environment variable
+const char* measure_env(const char* name) { return MPA_MEASURE ? std::getenv(name) : nullptr; }
 // rank 0 waits for remote completions of a launched-ahead epoch with one wait_words_kernel
 // (default) or, MPA_WAIT_VALUE_OPS=1, one hipStreamWaitValue64 per remote worker (round 1)
-const bool g_wait_value_ops = [] { const char* e = std::getenv("MPA_WAIT_VALUE_OPS"); return e && *e == '1'; }();
+const bool g_wait_value_ops = [] { const char* e = measure_env("MPA_WAIT_VALUE_OPS"); return e && *e == '1'; }();
 
 namespace {
 
@@ -87,8 +90,8 @@ bool env_off(const char* name) {
 
 // c5 launch grids (MPA_LSQB_GRID1 / MPA_LSQB_GRID2 override them for measurement)
 int lsqb_grid(int pass) {
-  static const int g1 = [] { const char* e = std::getenv("MPA_LSQB_GRID1"); return e ? std::max(8, std::atoi(e)) : kLsqbGrid1; }();
-  static const int g2 = [] { const char* e = std::getenv("MPA_LSQB_GRID2"); return e ? std::max(8, std::atoi(e)) : kLsqbGrid2; }();
+  static const int g1 = [] { const char* e = measure_env("MPA_LSQB_GRID1"); return e ? std::max(8, std::atoi(e)) : kLsqbGrid1; }();
+  static const int g2 = [] { const char* e = measure_env("MPA_LSQB_GRID2"); return e ? std::max(8, std::atoi(e)) : kLsqbGrid2; }();
   return pass == 1 ? g1 : g2;
 }
 
@@ -319,7 +322,7 @@ class HipComm final : public Comm {
     // front (the round-1 behaviour, for A/B measurements).
     int here_count = 0;
     for (const auto& w : w_) here_count += w.here;
-    const char* eager = std::getenv("MPA_EAGER_STREAMS");
+    const char* eager = measure_env("MPA_EAGER_STREAMS");
     if (eager && *eager == '1') {
       for (auto& w : w_)
         if (w.here) worker_stream(w);
@@ -336,20 +339,20 @@ class HipComm final : public Comm {
     // unset / 0: never pre-arm; 1: arm every eligible worker; 2: when a process serves one
     const char* arm = std::getenv("MPA_ARM");
     arm_mode_ = arm && *arm == '1' ? 1 : arm && *arm == '2' ? 2 : 0;
-    const char* cb = std::getenv("MPA_COORD_BATCH");
+    const char* cb = measure_env("MPA_COORD_BATCH");
     coord_batches_ = !(cb && *cb == '0');
     fused_tail_ = !env_off("MPA_TAIL");
-    { const char* e = std::getenv("MPA_LSQP_SHARE"); lsqp_share_ = e && *e == '1'; }
+    { const char* e = measure_env("MPA_LSQP_SHARE"); lsqp_share_ = e && *e == '1'; }
     {
-      const char* e = std::getenv("MPA_LSQP");
+      const char* e = measure_env("MPA_LSQP");  // the product's MPA_LSQP=0 is read where it applies
       lsqp8_ = e && *e == '8';
       lsqc_ = e && *e == 'c';
-      const char* la = std::getenv("MPA_LSQC_LA");
+      const char* la = measure_env("MPA_LSQC_LA");
       lsqc_la_ = la && *la == '1' ? 1 : 2;
     }
     hold_ok_ = !env_off("MPA_HOLD");
-    batch_gather_ = !env_off("MPA_GATHER");
-    if (const char* e = std::getenv("MPA_LSQP_PF")) lsqp_pfd_ = std::max(0, std::min(8, std::atoi(e)));
+    { const char* e = measure_env("MPA_GATHER"); batch_gather_ = !(e && *e == '0'); }
+    if (const char* e = measure_env("MPA_LSQP_PF")) lsqp_pfd_ = std::max(0, std::min(8, std::atoi(e)));
     const char* dbg = std::getenv("MPA_DEBUG");
     debug_ = dbg && *dbg == '1';
     if (debug_ && region_) {
@@ -368,7 +371,9 @@ class HipComm final : public Comm {
     }
     stop_timer();
     (void)hipDeviceSynchronize();
-    if (const char* d = MPA_MEASURE ? std::getenv("MPA_LSQF_DBG") : nullptr; d && (std::atoi(d) & 16)) lsqf_prof_dump();
+#if MPA_MEASURE
+    if (const char* d = measure_env("MPA_LSQF_DBG"); d && (std::atoi(d) & 16)) lsqf_prof_dump();
+#endif
     for (auto& w : w_) {
       if (w.slab) (void)hipFree(w.slab);
       if (w.wctr) (void)hipFree(w.wctr);
@@ -1325,24 +1330,26 @@ class HipComm final : public Comm {
       HIPCHECK(hipMemset(w.lsqb_ctr, 0, sizeof(uint32_t) * (kLsqbMaxSlices + 1)));
       HIPCHECK(hipDeviceSynchronize());
     }
-    if (ts.cols <= kLsqpMaxCols && !w.lsqp_slab) {
+    if (ts.cols <= kLsqpMaxCols && !w.lsqp_slab) {  // lsqp4 (and the measurement build's lsqp / lsqc)
       HIPCHECK(hipMalloc(&w.lsqp_slab, size_t(2) * kLsqpMaxGroups * 8 * 32 * 1024));
       const size_t nctr = size_t(2) * 8 * kLsqpCtrPerSlice + 8;  // + completions, lsqc ticket at +4
       HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqp_ctr), sizeof(uint32_t) * nctr));
       HIPCHECK(hipMemset(w.lsqp_ctr, 0, sizeof(uint32_t) * nctr));
-      const size_t xg = size_t(kLsqpMaxGroups) * 2 * kLsqcXR * 4 * 64 * 4 * sizeof(unsigned long long);
-      // the column pairs' exchange ring is rewritten every kLsqcXR blocks: in coarse-grained
-      // memory a reader's XCD L2 keeps serving its stale copy of a slot (sc1 loads bypass only
-      // L1), so the granules live in uncached device memory (MPA_LSQC_XG=fine / coarse: A/B)
-      {
-        const char* e = std::getenv("MPA_LSQC_XG");
+      // the column pairs' exchange ring (measurement build) is rewritten every kLsqcXR blocks:
+      // in coarse-grained memory a reader's XCD L2 keeps serving its stale copy of a slot (sc1
+      // loads bypass only L1), so the granules live in uncached device memory
+      // (MPA_LSQC_XG=fine / coarse: A/B)
+      if (MPA_MEASURE) {
+        const size_t xg = size_t(kLsqpMaxGroups) * 2 * kLsqcXR * 4 * 64 * 4 * sizeof(unsigned long long);
+        const char* e = measure_env("MPA_LSQC_XG");
         const unsigned fl = e && !std::strcmp(e, "fine") ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
         if (e && !std::strcmp(e, "coarse")) HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqc_xg), xg));
         else HIPCHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&w.lsqc_xg), xg, fl));
+        HIPCHECK(hipMemset(w.lsqc_xg, 0, xg));
       }
-      HIPCHECK(hipMemset(w.lsqc_xg, 0, xg));
       HIPCHECK(hipDeviceSynchronize());
     }
+    if (!MPA_MEASURE) return;  // the probe kernels' scratch (lsqq, lsqf): measurement build only
     if (ts.cols <= 2048 && !w.lsqq_ctr) {
       HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w.lsqq_ctr), sizeof(uint32_t) * 8));
       HIPCHECK(hipMemset(w.lsqq_ctr, 0, sizeof(uint32_t) * 8));
@@ -1361,7 +1368,7 @@ class HipComm final : public Comm {
 
   // workgroups per task in a least-squares launch of `ntasks` tasks
   int lsq_grid(const TaskSpec& ts, const HipWorker& w, int ntasks) const {
-    static const int env_grid = [] { const char* e = std::getenv("MPA_LSQ_GRID"); return e ? std::atoi(e) : 0; }();
+    static const int env_grid = [] { const char* e = measure_env("MPA_LSQ_GRID"); return e ? std::atoi(e) : 0; }();
     const int total = g_lsq_grid > 0 ? g_lsq_grid : env_grid > 0 ? env_grid : kDefaultLaunchGrid;
     const int rpw = lsq_rows_per_wave_iter(ts.dtype, int(ts.cols));
     const int64_t want = (ts.rows + 4 * rpw - 1) / (4 * rpw);
@@ -1754,7 +1761,7 @@ class HipComm final : public Comm {
   // the iterate-quarter single pass (lsqq_kernel.hip): cols <= 2048 on every task
   bool lsqq_enabled(const std::vector<int64_t>& ranks) const {
     if (!MPA_MEASURE) return false;  // a probe kernel of the measurement build (make MEASURE=1)
-    const char* e = std::getenv("MPA_LSQQ");
+    const char* e = measure_env("MPA_LSQQ");
     if (!e || *e != '1') return false;
     for (int64_t rank : ranks) {
       const TaskSpec& ts = tasks_[size_t(rank - 1)];
@@ -1764,9 +1771,9 @@ class HipComm final : public Comm {
   }
 
   bool lsqf_enabled(const std::vector<int64_t>& ranks) const {
-    // opt-in: the single-pass kernel is correct but, as measured, slower
-    // than the two passes
-    const char* e = std::getenv("MPA_LSQF");
+    // measurement build, opt-in: the single-pass kernel is correct but, as measured
+    // (DESIGN.md §10), slower than the two passes
+    const char* e = measure_env("MPA_LSQF");
     if (!e || *e != '1') return false;
     int P = 0;
     for (int64_t rank : ranks) {
@@ -1808,7 +1815,7 @@ class HipComm final : public Comm {
       LsqpBatch& b = L.halves;
       b.ntasks = int(ranks.size());
       b.pfd = lsqp_pfd_ >= 0 ? lsqp_pfd_ : (lsqp8_ ? 0 : 1);
-      { const char* d = MPA_MEASURE ? std::getenv("MPA_LSQP_DBG") : nullptr; b.dbg = d ? std::atoi(d) : 0; }
+      { const char* d = measure_env("MPA_LSQP_DBG"); b.dbg = d ? std::atoi(d) : 0; }
       // one workgroup per CU: 128 pairs (256 workgroups), dealt evenly over max(tasks,
       // share) tasks
       constexpr int target = 128;
@@ -1844,7 +1851,7 @@ class HipComm final : public Comm {
       L.quad = true;
       LsqqBatch& b = L.four;
       b.ntasks = int(ranks.size());
-      { const char* d = std::getenv("MPA_LSQQ_DBG"); b.dbg = d ? std::atoi(d) : 0; }
+      { const char* d = measure_env("MPA_LSQQ_DBG"); b.dbg = d ? std::atoi(d) : 0; }
       // one 512-thread workgroup per CU: 64 quads (grid 256, a multiple of 32 so that each
       // quad's members share an XCD), dealt evenly over the tasks
       constexpr int target = 64;
@@ -1881,8 +1888,8 @@ class HipComm final : public Comm {
       b.err = err_dev_;
       b.spin_ticks = spin_ticks();
       // probe modes and the phase-1 lead: measurement build only (make MEASURE=1)
-      { const char* d = MPA_MEASURE ? std::getenv("MPA_LSQF_DBG") : nullptr; b.dbg = d ? std::atoi(d) : 0; }
-      { const char* d = MPA_MEASURE ? std::getenv("MPA_LSQF_LAG") : nullptr; b.lag = d ? std::atoi(d) : 4; }
+      { const char* d = measure_env("MPA_LSQF_DBG"); b.dbg = d ? std::atoi(d) : 0; }
+      { const char* d = measure_env("MPA_LSQF_LAG"); b.lag = d ? std::atoi(d) : 4; }
       b.P = int((tasks_[size_t(ranks[0] - 1)].cols + kLsqfSlice - 1) / kLsqfSlice);
       // one workgroup per CU: groups of P, as many as keep the grid a multiple of 8 P (the
       // groups form inside an XCD, 8 XCDs), dealt evenly over the tasks
@@ -1985,8 +1992,8 @@ class HipComm final : public Comm {
     HIPCHECK(b.pair ? (b.cpair ? launch_lsqc(b.halves, s) : b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
                     : b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #else
-    HIPCHECK(b.pair ? (b.cpair ? launch_lsqc(b.halves, s) : b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
-                    : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
+    // the product carries the iterate-halves single pass and the two passes only
+    HIPCHECK(b.pair ? launch_lsqp4(b.halves, s) : launch_lsqb(b.two, s));
 #endif
     if (timed) {
       HIPCHECK(hipEventRecord(tl.stop, s));

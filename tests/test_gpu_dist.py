@@ -72,9 +72,7 @@ def test_lsqb_two_processes(built, monkeypatch, arm):
     ([0, 1], {"MPA_FUSE": "0"}),                          # the unfused loop
     ([0, 1, 1], {"MPA_XGMI": "0"}),                       # payloads through the host mailbox
     ([0, 1], {"MPA_XGMI": "0", "MPA_ARM": "2"}),          # ... pre-armed
-    ([0, 1, 1], {"MPA_WAIT_VALUE_OPS": "1"}),             # one stream wait per remote worker (round 1)
-    ([0, 1, 1, 1], {"MPA_GATHER": "0"}),                  # servers launch what one doorbell scan found
-])
+])  # (MPA_WAIT_VALUE_OPS / MPA_GATHER, A/B switches, exist in the measurement build only)
 def test_lsq_descent_two_processes(built, placement, env):
     import torch
     if not torch.cuda.is_available():
