@@ -1,0 +1,275 @@
+// HipComm, worker processes (N > 1): the doorbell loop of mpa_comm_serve (the
+// reference's worker_main, examples/iterative_example.jl:55-82), pre-armed tasks and their
+// cancellation, the HIP IPC device-memory payload path over xGMI and the host-mailbox fallback.
+#include "hip_transport.hpp"
+
+namespace mpa {
+
+void HipComm::serve() {
+  if (role_ != SERVER) fail(MPA_ERROR, "mpa_comm_serve is for worker processes (rank != 0)");
+  ShmHeader* h = region_->header();
+  const uint64_t gen0 = __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE);
+  const auto t0 = Clock::now();
+  struct Disarm {
+    HipComm* c;
+    ~Disarm() { c->disarm_all(); }
+  } disarm_guard{this};
+  std::vector<int64_t> fresh;
+  for (int64_t r = 1; r <= nworkers_; ++r)
+    if (w_[size_t(r - 1)].here && server_path(r) && armable(r)) arm(r);
+  for (uint64_t spins = 0;; ++spins) {
+    if (__atomic_load_n(&h->shutdown, __ATOMIC_ACQUIRE) || __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE) != gen0) break;
+    fresh.clear();
+    bool progress = false;
+    for (int64_t r = 1; r <= nworkers_; ++r) {
+      HipWorker& w = w_[size_t(r - 1)];
+      if (!w.here) continue;
+      if (!w.path_known) {
+        if (server_path(r)) {
+          progress = true;
+          if (armable(r)) arm(r);
+        }
+        continue;
+      }
+      if (w.armed) {
+        if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) continue;
+        // the armed task ran: check what rank 0 posted against what it was armed for
+        w.armed = false;
+        check_task(r, tasks_[size_t(r - 1)], size_t(w.box->msg_bytes), size_t(w.box->reply_bytes));
+        progress = true;
+        if (armable(r)) arm(r);
+        continue;
+      }
+      const unsigned long long db = __atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE);
+      if (db == w.seq) continue;
+      if (db != w.seq + 1) fail(MPA_ERROR, "mailbox protocol: worker %lld doorbell %llu after %llu", (long long)r, db, w.seq);
+      if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) != w.seq)
+        fail(MPA_ERROR, "mailbox protocol: worker %lld posted while busy", (long long)r);
+      w.seq = db;
+      w.sl = size_t(w.box->msg_bytes);
+      w.rl = size_t(w.box->reply_bytes);
+      check_task(r, tasks_[size_t(r - 1)], w.sl, w.rl);
+      w.x = w.xslot;
+      w.out = reply_dst(w);
+      fresh.push_back(r);
+    }
+    if (!fresh.empty()) {
+      // rank 0's exchange kernel rings a flush's doorbells one after another: a scan that
+      // caught the first ones looks again for ~2 us before launching, so the flush's tasks
+      // here go out as one batch (the c2 N = 2 trace showed them split over two launches)
+      if (batch_gather_) {
+        const auto g0 = Clock::now();
+        while (std::chrono::duration<double, std::micro>(Clock::now() - g0).count() < 2.0) {
+          for (int64_t r = 1; r <= nworkers_; ++r) {
+            HipWorker& w = w_[size_t(r - 1)];
+            if (!w.here || !w.path_known || w.armed || std::find(fresh.begin(), fresh.end(), r) != fresh.end()) continue;
+            const unsigned long long db = __atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE);
+            if (db != w.seq + 1 || __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) != w.seq) continue;
+            w.seq = db;
+            w.sl = size_t(w.box->msg_bytes);
+            w.rl = size_t(w.box->reply_bytes);
+            check_task(r, tasks_[size_t(r - 1)], w.sl, w.rl);
+            w.x = w.xslot;
+            w.out = reply_dst(w);
+            fresh.push_back(r);
+          }
+          int postable = 0;  // workers here that could still be posted (not busy, not armed)
+          for (int64_t r = 1; r <= nworkers_; ++r) {
+            const HipWorker& w = w_[size_t(r - 1)];
+            postable += w.here && w.path_known && !w.armed &&
+                        (std::find(fresh.begin(), fresh.end(), r) != fresh.end() ||
+                         __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) == w.seq);
+          }
+          if (int(fresh.size()) >= postable) break;  // every worker that could be posted is
+          __builtin_ia32_pause();
+        }
+        std::sort(fresh.begin(), fresh.end());
+      }
+      if (timing_) reap_timing(false);
+      launch_tasks(fresh, /*staged=*/true);
+    } else if (!progress) {
+      if ((spins & 0xFFF) == 0xFFF) watchdog(t0, /*timeout=*/false);
+      __builtin_ia32_pause();
+    }
+  }
+}
+
+bool HipComm::armable(int64_t rank) const {
+  const TaskSpec& ts = tasks_[size_t(rank - 1)];
+  if (arm_mode_ == 0 || !((ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty()))
+    return false;
+  if (arm_mode_ == 1) return true;
+  int here = 0;
+  for (const auto& w : w_) here += w.here;
+  return here == 1;
+}
+
+void HipComm::arm(int64_t rank) {
+  HipWorker& w = w_[size_t(rank - 1)];
+  const TaskSpec& ts = tasks_[size_t(rank - 1)];
+  const unsigned long long s = w.seq + 1;
+  w.arm_sbase = w.lsqb_sbase;
+  w.arm_tbase = w.lsqb_tbase;
+  w.arm_fsbase = w.lsqf_sbase;
+  w.arm_ftbase = w.lsqf_tbase;
+  HIPCHECK(hipStreamWaitValue64(worker_stream(w), w.box_door_dev, s, hipStreamWaitValueGte, ~0ull));
+  w.seq = s;
+  w.sl = task_msg_bytes(ts);
+  w.rl = w.sl * (ts.kind == MPA_TASK_LSQ_BATCH ? 2 : 1);
+  w.x = w.xslot;
+  w.out = reply_dst(w);
+  if (!w.path_dev) {  // host mailbox: stage the message into the device slot first
+    ExchangeBuilder xb(ticket_, &ticket_count_, w.stream);
+    xb.copy(w.box_msg_dev, w.xslot, w.sl);
+    xb.launch();
+  }
+  double bytes = 0;
+  if (ts.kind == MPA_TASK_LSQ) {
+    LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes, armed_share());
+    b.t[0].go = w.cancel_dev;
+    enqueue_lsq(b, ts.dtype, int(ts.cols), w.stream, bytes, rank);
+  } else {
+    LsqbLaunch b = build_lsqb_batch({rank}, &bytes, armed_share());
+    b.set_go(w.cancel_dev);
+    enqueue_lsqb(b, w.stream, bytes, rank);
+  }
+  w.armed = true;
+}
+
+void HipComm::disarm_all() {
+  if (role_ != SERVER) return;
+  for (int64_t r = 1; r <= nworkers_; ++r) {
+    HipWorker& w = w_[size_t(r - 1)];
+    if (!w.here || !w.armed) continue;
+    unsigned long long expect = w.seq - 1;
+    bool cancelled = false;
+    if (__atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE) < w.seq) {
+      __atomic_store_n(w.cancel_host, w.seq, __ATOMIC_SEQ_CST);
+      cancelled = __atomic_compare_exchange_n(&w.box->doorbell, &expect, w.seq | kCancelBit, false, __ATOMIC_SEQ_CST,
+                                              __ATOMIC_SEQ_CST);
+    }
+    (void)hipStreamSynchronize(w.stream);
+    if (cancelled) {
+      unsigned long long c2 = w.seq | kCancelBit;  // restore unless rank 0 rang meanwhile
+      __atomic_compare_exchange_n(&w.box->doorbell, &c2, w.seq - 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+    }
+    __atomic_store_n(w.cancel_host, 0ull, __ATOMIC_SEQ_CST);
+    if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) {  // it did not run
+      w.seq -= 1;
+      w.lsqb_sbase = w.arm_sbase;
+      w.lsqb_tbase = w.arm_tbase;
+      w.lsqf_sbase = w.arm_fsbase;
+      w.lsqf_tbase = w.arm_ftbase;
+      void_timing(r);
+    }
+    w.armed = false;
+  }
+}
+
+void* HipComm::ipc_alloc(size_t bytes, char* handle, volatile uint32_t* state) {
+  void* p = nullptr;
+  if (xgmi_ && hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) == hipSuccess) {
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, p) == hipSuccess) {
+      std::memcpy(handle, &h, sizeof(h));
+      __atomic_store_n(state, kIpcOk, __ATOMIC_RELEASE);
+      return p;
+    }
+    (void)hipGetLastError();
+    std::fprintf(stderr, "[mpa] hipIpcGetMemHandle failed: worker payloads use the host mailbox\n");
+    (void)hipFree(p);
+    p = nullptr;
+  }
+  (void)hipGetLastError();
+  HIPCHECK(hipMalloc(&p, bytes));
+  __atomic_store_n(state, kIpcFailed, __ATOMIC_RELEASE);
+  return p;
+}
+
+void* HipComm::ipc_open(const char* handle, int peer_dev) {
+  if (peer_dev != dev_) {
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, dev_, peer_dev) != hipSuccess || !can) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    const hipError_t e = hipDeviceEnablePeerAccess(peer_dev, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    (void)hipGetLastError();
+  }
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  void* p = nullptr;
+  if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void HipComm::decide_path(int64_t rank) {
+  HipWorker& w = w_[size_t(rank - 1)];
+  BoxHeader* b = w.box;
+  const auto t0 = Clock::now();
+  for (uint64_t spins = 0; __atomic_load_n(&b->msg_ipc, __ATOMIC_ACQUIRE) == kIpcPending ||
+                           __atomic_load_n(&b->reply_open, __ATOMIC_ACQUIRE) == kIpcPending;
+       ++spins) {
+    if ((spins & 0xFFF) == 0xFFF) watchdog(t0);
+    __builtin_ia32_pause();
+  }
+  uint32_t mode = kPathHost;
+  if (b->msg_ipc == kIpcOk && b->reply_open == kIpcOk && b->reply_ipc == kIpcOk) {
+    w.peer_msg = static_cast<uint8_t*>(ipc_open(b->msg_handle, b->server_dev));
+    if (w.peer_msg) mode = kPathDevice;
+  }
+  if (mode != kPathDevice && xgmi_)
+    std::fprintf(stderr, "[mpa] worker %lld: device payload path unavailable, using the host mailbox\n",
+                 (long long)rank);
+  w.path_dev = mode == kPathDevice;
+  w.path_known = true;
+  __atomic_store_n(&b->mode, mode, __ATOMIC_RELEASE);
+}
+
+bool HipComm::server_path(int64_t rank) {
+  HipWorker& w = w_[size_t(rank - 1)];
+  if (w.path_known) return true;
+  BoxHeader* b = w.box;
+  if (__atomic_load_n(&b->reply_open, __ATOMIC_ACQUIRE) == kIpcPending) {
+    const uint32_t ri = __atomic_load_n(&b->reply_ipc, __ATOMIC_ACQUIRE);
+    if (ri == kIpcPending) return false;
+    if (ri == kIpcOk && b->msg_ipc == kIpcOk) w.peer_reply = static_cast<uint8_t*>(ipc_open(b->reply_handle, b->coord_dev));
+    __atomic_store_n(&b->reply_open, w.peer_reply ? kIpcOk : kIpcFailed, __ATOMIC_RELEASE);
+  }
+  const uint32_t mode = __atomic_load_n(&b->mode, __ATOMIC_ACQUIRE);
+  if (mode == kPathPending) return false;
+  if (mode == kPathDevice && !w.peer_reply) fail(MPA_ERROR, "worker %lld: device path chosen without a reply inbox", (long long)rank);
+  w.path_dev = mode == kPathDevice;
+  w.path_known = true;
+  return true;
+}
+
+void HipComm::stage_in(const std::vector<int64_t>& ranks, hipStream_t s) {
+  ExchangeBuilder xb(ticket_, &ticket_count_, s);
+  for (int64_t rank : ranks) {
+    const HipWorker& w = w_[size_t(rank - 1)];
+    if (w.path_dev) continue;  // rank 0 stored the message into the device slot itself
+    if (debug_) {
+      std::fprintf(stderr, "[mpa role %d] stage-in worker %lld: %zu bytes %p -> %p\n", int(role_), (long long)rank, w.sl,
+                   (void*)w.box_msg_dev, (void*)w.xslot);
+      describe("box msg", w.box_msg_dev);
+      describe("xslot", w.xslot);
+    }
+    xb.copy(w.box_msg_dev, w.xslot, w.sl);
+  }
+  xb.launch();
+  if (debug_) {
+    const hipError_t e = hipStreamSynchronize(s);
+    std::fprintf(stderr, "[mpa role %d] stage-in done: %s\n", int(role_), hipGetErrorString(e));
+    std::fflush(stderr);
+  }
+}
+
+}  // namespace mpa

@@ -1,0 +1,708 @@
+// The HIP transport's shared declarations: the HipComm class (a Comm whose workers are
+// device tasks), its worker records, the exchange-kernel builder and the process-wide stream
+// pool.  The class is implemented in three units:
+//   transport_hip.cpp  the coordinator: the per-call protocol of the state machine, the
+//                      native descent loop's epoch step (launch-ahead, fused tail), the gate
+//   hip_server.cpp     worker processes (N > 1): doorbell serving, pre-armed tasks, HIP IPC
+//   hip_launch.cpp     task launches: batching, kernel arguments, straggler timer, timing
+// See transport_hip.cpp for the mapping onto the reference's MPI verbs.
+#pragma once
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+
+#include "comm.hpp"
+#include "kernels.hpp"
+#include "shm.hpp"
+
+#ifndef MPA_MEASURE
+#define MPA_MEASURE 0
+#endif
+
+namespace mpa {
+
+#define HIPCHECK(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) fail(MPA_DEVICE_ERROR, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+extern int g_lsq_grid;  // mpa_tune("lsq_grid", G): workgroups per least-squares launch (0 = default)
+// A/B switches of the measurement build only (make MEASURE=1): the product reads none of
+// them, so the shipped behaviour cannot be switched off by an environment variable
+inline const char* measure_env(const char* name) { return MPA_MEASURE ? std::getenv(name) : nullptr; }
+// rank 0 waits for remote completions of a launched-ahead epoch with one wait_words_kernel
+// (default) or, MPA_WAIT_VALUE_OPS=1, one hipStreamWaitValue64 per remote worker (round 1)
+extern const bool g_wait_value_ops;
+
+using Clock = std::chrono::steady_clock;
+// workgroups per least-squares launch: 192 (24 per XCD, 3/4 of the CUs) streams the c2
+// batch at 7.1-7.2 TB/s against 6.7-6.8 at 512 and 7.0 at 256 (profiles/r01_tune_sweep4_grid.jsonl,
+// same-box bench A/B in profiles/r01_lsq_grid_ab.txt: c2 +6-7 %, c3/c4 unchanged); the read
+// probe (mpa_read_bandwidth) shows the same shape: fewer, longer streams read faster
+constexpr int kDefaultLaunchGrid = 192;
+constexpr int kWideResidGrid = 1024;  // wide rows: pass-1 workgroups per launch (a wave per row)
+constexpr int kSlabGridCap = kLsqMaxGrid;  // most workgroups a single task may be given
+constexpr int kLaunchStreams = 2;
+// batched multi-iterate task: pass-1 / pass-2 workgroups per launch (= resident: 1 x 512 /
+// 2 x 256 threads per CU by VGPRs), and the most row ranges a pass-2 task is split into
+constexpr int kLsqbGrid1 = 512;  // two 8-wave workgroups per CU: pass 1 4.74-4.88 -> 5.11 TB/s (profiles/r01_lsqb_grid.txt)
+constexpr int kLsqbGrid2 = 512;
+constexpr int kLsqbRangeCap = 128;
+constexpr int kLsqfGrid = 256;  // single-pass batched launch: one 768-thread workgroup per CU
+constexpr size_t kLsqfCtrBytes = 64 + 16 * sizeof(unsigned long long);
+
+inline bool env_off(const char* name) {
+  const char* e = std::getenv(name);
+  return e && *e == '0';
+}
+
+// c5 launch grids (MPA_LSQB_GRID1 / MPA_LSQB_GRID2 override them for measurement)
+inline int lsqb_grid(int pass) {
+  static const int g1 = [] { const char* e = measure_env("MPA_LSQB_GRID1"); return e ? std::max(8, std::atoi(e)) : kLsqbGrid1; }();
+  static const int g2 = [] { const char* e = measure_env("MPA_LSQB_GRID2"); return e ? std::max(8, std::atoi(e)) : kLsqbGrid2; }();
+  return pass == 1 ? g1 : g2;
+}
+
+// Process-wide pool of CU-masked streams (hip_launch.cpp): communicators come and go
+// (tests create many), but the HSA queues behind their streams are a bounded hardware
+// resource, so a destroyed comm returns its streams to the pool and the next comm reuses them.
+hipStream_t make_queue_stream(int device);
+void release_queue_stream(int device, hipStream_t s);
+
+struct HipWorker {
+  bool here = true;     // its tasks run in this process
+  bool remote = false;  // coordinator's view of a worker served by another process
+  hipStream_t stream = nullptr;
+  unsigned long long seq = 0;  // coordinator: tasks posted; server: tasks served
+  void* slab = nullptr;
+  int slab_grid = 0;
+  size_t slab_bytes = 0;
+  uint32_t* wctr = nullptr;  // wide rows (lsqw_kernel.hip): per-slice tree + completion counters
+  // batched multi-iterate task (lsqb_kernel.hip): residual scratch, pass-2 partials,
+  // counters and their running totals
+  void* lsqb_R = nullptr;
+  size_t lsqb_R_bytes = 0;
+  void* lsqb_slab = nullptr;
+  size_t lsqb_slab_bytes = 0;
+  uint32_t* lsqb_ctr = nullptr;
+  uint32_t lsqb_sbase = 0, lsqb_tbase = 0;
+  // single-pass variant (lsqf_kernel.hip): exchange ring, its flags, counters
+  // ([kLsqfMaxP] slices, [1] completions, [1] group tickets) and their running totals
+  void* lsqf_x = nullptr;
+  unsigned long long* lsqf_flag = nullptr;
+  uint32_t* lsqf_ctr = nullptr;
+  uint32_t* lsqq_ctr = nullptr;  // quad kernel: [4] member arrivals, [4] completions (self-resetting)
+  // pair single pass (lsqp_kernel.hip): G partials and tree counters (self-resetting)
+  void* lsqp_slab = nullptr;
+  uint32_t* lsqp_ctr = nullptr;  // [2][8][kLsqpCtrPerSlice] tree, [1] completions, then the lsqc ticket
+  unsigned long long* lsqc_xg = nullptr;  // column pairs: exchange granules
+  uint32_t lsqf_sbase = 0, lsqf_tbase = 0;
+  // current task
+  int64_t slot = -1;
+  const uint8_t* x = nullptr;
+  uint8_t* out = nullptr;
+  size_t sl = 0, rl = 0;
+  unsigned long long* flag_host = nullptr;  // completion word, host view
+  unsigned long long* flag_dev = nullptr;   // the same word, device view
+  // mailbox (remote worker on the coordinator / served worker in a worker process)
+  BoxHeader* box = nullptr;
+  uint8_t* box_msg_dev = nullptr;
+  uint8_t* box_reply_dev = nullptr;
+  unsigned long long* box_door_dev = nullptr;
+  uint8_t* xslot = nullptr;  // server: the worker's device message slot
+  // device-memory (xGMI) payload path (shm.hpp kPathDevice): coordinator: the server's
+  // message slot opened by IPC, and its own reply inbox; server: rank 0's inbox opened
+  bool path_known = false, path_dev = false;
+  uint8_t* peer_msg = nullptr;
+  uint8_t* reply_inbox = nullptr;
+  uint8_t* peer_reply = nullptr;
+  // server, pre-armed task (serve()): armed = task `seq` is queued behind its doorbell;
+  // cancel word (host-pinned, device view) of the armed task; counter bases to restore
+  // if cancelled
+  bool armed = false;
+  unsigned long long* cancel_host = nullptr;
+  unsigned long long* cancel_dev = nullptr;
+  // coordinator, launch-ahead: the next post / harvest of this worker is already enqueued
+  bool preposted = false, preharvest = false;
+  uint32_t arm_sbase = 0, arm_tbase = 0, arm_fsbase = 0, arm_ftbase = 0;
+};
+
+// Accumulates copy items and doorbells into as few exchange launches as fit the kernel
+// argument (kMaxCopies / kMaxDoorbells per launch), in order.
+class ExchangeBuilder {
+ public:
+  ExchangeBuilder(uint32_t* ticket, uint32_t* ticket_count, hipStream_t s)
+      : ticket_(ticket), count_(ticket_count), s_(s) {
+    reset();
+  }
+  void reserve(int copies, int doors) {
+    if (a_.ncopy + copies > kMaxCopies || a_.ndoor + doors > kMaxDoorbells) launch();
+  }
+  void copy(const uint8_t* src, uint8_t* dst, uint64_t bytes) {
+    if (bytes == 0) return;
+    reserve(1, 0);
+    CopyItem& c = a_.c[a_.ncopy];
+    c.src = src;
+    c.dst = dst;
+    c.bytes = bytes;
+    a_.block0[a_.ncopy] = blocks_;
+    blocks_ += int((bytes + kPart - 1) / kPart);
+    a_.ncopy += 1;
+    a_.block0[a_.ncopy] = blocks_;
+  }
+  void door(unsigned long long* addr, unsigned long long value) {
+    reserve(0, 1);
+    a_.door[a_.ndoor] = addr;
+    a_.doorval[a_.ndoor] = value;
+    a_.ndoor += 1;
+  }
+  void launch() {
+    if (a_.ncopy == 0 && a_.ndoor == 0) return;
+    const int grid = blocks_ > 0 ? blocks_ : 1;
+    if (a_.ndoor > 0) {
+      a_.ticket = ticket_;
+      a_.ticket_base = *count_;
+      *count_ += uint32_t(grid);
+    }
+    HIPCHECK(launch_exchange(a_, s_));
+    reset();
+  }
+
+ private:
+  static constexpr uint64_t kPart = 64 * 1024;
+  void reset() {
+    a_ = ExchangeArgs{};
+    a_.part = kPart;
+    blocks_ = 0;
+  }
+  ExchangeArgs a_{};
+  int blocks_ = 0;
+  uint32_t* ticket_;
+  uint32_t* count_;
+  hipStream_t s_;
+};
+
+class HipComm final : public Comm {
+ public:
+  enum Role { SOLO, COORD, SERVER };
+
+  HipComm(int64_t n, const int* devices, const int* placement, int my_rank, ShmRegion* region);
+
+  ~HipComm() override;
+
+  int transport() const override { return MPA_TRANSPORT_HIP; }
+  void set_stream(hipStream_t s) { coord_ = s; }
+  hipStream_t stream() const { return coord_; }
+
+  void begin_call(const CallBufs& b) override {
+    if (role_ == SERVER) fail(MPA_ERROR, "asyncmap!/waitall! run on rank 0; this process serves workers (mpa_comm_serve)");
+    b_ = b;
+    call_posts_.clear();
+  }
+
+  void post(int64_t i, int64_t rank, int64_t tag) override;
+
+  void harvest(int64_t i, int64_t rank) override;
+
+  bool test(int64_t i, int64_t rank) override {
+    (void)i;
+    return done(rank);
+  }
+
+  int64_t waitany(int64_t n, const int64_t* ranks, const uint8_t* live) override;
+
+  void waitall(int64_t n, const int64_t* ranks, const uint8_t* live) override;
+
+  void flush() override;
+
+  void end_call() override {
+    may_hold_ = false;
+    if (!defer_end_) flush();
+  }
+
+  // A stale worker's re-dispatch (pool.cpp, the wait loop): its message copies and the
+  // stale harvest go out now, its task launch is HELD (undelayed least-squares tasks only)
+  // and joins the next flush's batch, or is launched when a wait would block.  On one GPU
+  // the coordinator stream runs launches in order, so a re-dispatch enqueued behind the
+  // running batch starts when that batch ends either way; held, it runs INSIDE the next
+  // epoch's batched launch instead of alone before it (c5, nwait 7 of 8: one 8-task launch
+  // per epoch instead of a 1-task launch and a 7-task launch, profiles/r02_c5_hold_ab.txt).
+  // The pool's state machine is unchanged; MPA_HOLD=0 launches re-dispatches at once.
+  void flush_stale() override {
+    hold_next_ = hold_ok_;
+    flush();
+    hold_next_ = false;
+  }
+  void set_wait_hold(bool may_hold) override { may_hold_ = may_hold; }
+  void release_held();
+
+  // ---- the native descent loop (capi.cpp descent_loop) ----
+  // The iterate update between two asyncmap! calls, folded into the next flush (one epoch
+  // kernel: harvests, update, dispatch copies, doorbells) instead of its own launches.
+  struct UpdateSpec {
+    int dtype = MPA_F32;  // of x and of the recv chunks
+    int64_t elems = 0;
+    std::vector<double> w;
+    double eta = 0;
+    void* x = nullptr;
+    uint16_t* mirror = nullptr;  // bf16 copy of x; the message when msg_bf16
+    bool msg_bf16 = false;
+  };
+  int payload_path(int64_t rank) const {
+    if (rank < 1 || rank > nworkers_) return 0;
+    const HipWorker& w = w_[size_t(rank - 1)];
+    return w.remote && w.path_known ? (w.path_dev ? int(kPathDevice) : int(kPathHost)) : 0;
+  }
+  // end_call() leaves the call's harvests pending (they join the next flush's epoch kernel)
+  void set_defer_end_flush(bool on) {
+    defer_end_ = on;
+    if (!on) tail_next_ = tail_pending_ = false;  // the descent loop ended (or failed)
+  }
+  void stage_update(const UpdateSpec& u);
+  // Launch-ahead (integer nwait == n): the call returns only once all n tasks it posts have
+  // completed fresh, so the next epoch is fully determined before this call's waits begin:
+  // harvest all n, update with weight 1 each, re-post all n.  The phase-2 flush of such a
+  // call enqueues that next epoch (epoch kernel + tasks) right behind this one; the next
+  // call then finds its posts already enqueued.  `epochs_left` = calls still to come.
+  void set_ahead(int64_t epochs_left, const UpdateSpec& pred) {
+    ahead_left_ = epochs_left;
+    ahead_pred_ = pred;
+  }
+
+  uint64_t now_ns() override {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count());
+  }
+
+  int64_t tasks_done(int64_t rank) override {
+    return int64_t(__atomic_load_n(w_[size_t(rank - 1)].flag_host, __ATOMIC_ACQUIRE));
+  }
+
+  void shutdown() override;
+
+  void on_task_changed(int64_t rank) override;
+
+  // ---- worker process: watch the doorbells of the workers served here ----
+  // Least-squares workers without a delay schedule are PRE-ARMED: their next task is
+  // already queued on the worker's own stream behind hipStreamWaitValue64 on the mailbox
+  // doorbell, so the GPU starts it when rank 0's exchange kernel rings (3.2 us ring -> task
+  // start, against 13.4 us for host polling + launch; profiles/r01_probe_waitvalue.txt).
+  // Other workers (the reference's test programs, injected delays) are launched by this
+  // thread when it sees their doorbell.  serve() returns at pause / shutdown after
+  // disarming: the pending waits are released with kCancelBit and their tasks return
+  // without computing or publishing.
+  void serve();
+
+  // ---- pre-armed tasks (server) ----
+  // Off by default (MPA_ARM=2: where a process serves ONE worker; MPA_ARM=1: every eligible
+  // worker).  The armed launch saves the host's doorbell poll + launch (3.2 vs 13.4 us ring ->
+  // start) but its task ran 7-15x longer than the same task launched by the host: every
+  // workgroup reads the host-memory go word before it starts (one-GPU N = 2 rehearsal, c1:
+  // 134 us with every lane reading, 73 us with one lane per wave, 9.6 us host-launched;
+  // 106 vs 48 us per epoch; c2 with 4 armed workers 1.20 vs 0.74 ms; profiles/r02_arm_go_word.txt).
+  // With several workers the host-launched path also batches them into one launch
+  // (profiles/r01_n2_arm_ab.txt).
+  bool armable(int64_t rank) const;
+  // local workers that serve() pre-arms: each armed launch gets its share of the launch grid
+  int armed_share() const {
+    int k = 0;
+    for (int64_t r = 1; r <= nworkers_; ++r) k += w_[size_t(r - 1)].here && armable(r);
+    return k > 0 ? k : 1;
+  }
+
+  // message / reply bytes of a task as armed (the post is checked against them afterwards)
+  static size_t task_msg_bytes(const TaskSpec& ts) {
+    return ts.kind == MPA_TASK_LSQ_BATCH ? size_t(ts.cols) * size_t(ts.k) * 2
+                                         : size_t(ts.cols) * (ts.dtype == MPA_F64 ? 8 : 4);
+  }
+
+  // queue task seq+1 of `rank` on its stream: wait for the doorbell, stage the message and
+  // the doorbell value (the task's go word), run the task
+  void arm(int64_t rank);
+
+  // release every pending armed wait: a task whose doorbell rank 0 has not rung is
+  // cancelled (cancel word := its seq, then doorbell := seq | kCancelBit to release the
+  // wait; both restored once the stream has drained), one already rung completes.  A task
+  // cancelled in a race with rank 0's ring did not run: its doorbell is served by the next
+  // serve() session (seq rolled back).
+  void disarm_all();
+
+  void pause_servers() {
+    if (role_ != COORD) fail(MPA_ERROR, "only rank 0 of a multi-process communicator pauses its servers");
+    __atomic_fetch_add(&region_->header()->gen, 1ull, __ATOMIC_RELEASE);
+  }
+
+ private:
+  struct Harvest {
+    int64_t slot, rank;
+  };
+
+  void add_harvest(ExchangeBuilder& xb, const Harvest& h) {
+    const HipWorker& w = w_[size_t(h.rank - 1)];
+    const uint8_t* src = w.remote ? reply_src(w) : b_.irecvbuf + size_t(h.slot) * b_.rl;
+    xb.copy(src, b_.recvbuf + size_t(h.slot) * b_.rl, b_.rl);
+  }
+
+  // tasks of the workers served here among `posted`, behind the exchange / epoch kernel
+  void launch_local(const std::vector<int64_t>& posted);
+
+  // the update as its own launch (the unfused path)
+  void launch_update(const UpdateSpec& u);
+
+  bool fused_ok(const UpdateSpec& u, const std::vector<int64_t>& posted) const;
+
+  // the epoch step can ride as the fused tail of the launch of `posted`: one batched
+  // least-squares launch on the coordinator stream (local, undelayed, same shape, the
+  // update's dtype), no doorbells, no bf16 mirror
+  bool tail_fits(const std::vector<int64_t>& posted, const UpdateSpec& u) const;
+
+  // ONE epoch kernel: harvests [0, before) of `hv`, the update, harvests [before, end), the
+  // dispatch copies of the posts (isendbuf slot; mailbox + doorbell for a remote worker)
+  void emit_epoch(const std::vector<Harvest>& hv, size_t before, const std::vector<int64_t>& posted,
+                  const UpdateSpec& u, hipStream_t s);
+
+  // the arguments of one epoch step (no doorbell ticket yet)
+  EpochArgs epoch_args(const std::vector<Harvest>& hv, size_t before, const std::vector<int64_t>& posted,
+                       const UpdateSpec& u) const;
+
+  // enqueue the next epoch of an await-all call (set_ahead), once per call, when this
+  // call has posted every worker of the pool
+  void maybe_ahead();
+
+  // ---- device-memory (xGMI) payload path (shm.hpp kPathDevice) ----
+  // A fine-grained device buffer exported by a HIP IPC handle into `handle`; `state` tells
+  // the other process whether it may open it.  Falls back to a plain allocation (state
+  // kIpcFailed, payloads then go through the host mailbox) if fine-grained memory or IPC is
+  // unavailable, or with MPA_XGMI=0.
+  void* ipc_alloc(size_t bytes, char* handle, volatile uint32_t* state);
+
+  void* ipc_open(const char* handle, int peer_dev);
+
+  // coordinator, first post to a remote worker: once the server has exported its message
+  // slot and opened our reply inbox, open its slot and fix the path for good
+  void decide_path(int64_t rank);
+
+  // server: open rank 0's reply inbox once it is exported; true once rank 0 fixed the path
+  bool server_path(int64_t rank);
+
+  // where rank 0 stores a remote worker's message / reads its reply
+  uint8_t* msg_dst(const HipWorker& w) const { return w.path_dev ? w.peer_msg : w.box_msg_dev; }
+  const uint8_t* reply_src(const HipWorker& w) const { return w.path_dev ? w.reply_inbox : w.box_reply_dev; }
+  // where a served worker's task writes its reply
+  uint8_t* reply_dst(const HipWorker& w) const { return w.path_dev ? w.peer_reply : w.box_reply_dev; }
+
+  bool done(int64_t rank) const {
+    const HipWorker& w = w_[size_t(rank - 1)];
+    return __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) >= w.seq && gate_open(rank, w.seq);
+  }
+
+  int64_t counter(const char* name) const override;
+
+  // gated replay hooks (gate.cpp): the coordinator's view of its workers
+  bool gate_supported() const override { return role_ != SERVER; }
+  uint64_t gate_posted(int64_t rank) override { return w_[size_t(rank - 1)].seq; }
+  uint64_t gate_finished(int64_t rank) override { return __atomic_load_n(w_[size_t(rank - 1)].flag_host, __ATOMIC_ACQUIRE); }
+  void gate_launch(int64_t rank) override {
+    // a held re-dispatch the schedule completes: launch it (with the rest of the held batch)
+    if (std::find(held_.begin(), held_.end(), rank) != held_.end()) release_held();
+  }
+  void gate_poll(double waited_s) override {
+    watchdog(Clock::now(), /*timeout=*/false);
+    if (timeout_s_ > 0 && waited_s > timeout_s_)
+      fail(MPA_DEVICE_ERROR, "gated replay: waited more than %.0f s for a released task (MPA_WAIT_TIMEOUT_S)", timeout_s_);
+  }
+
+  unsigned device_error() const {
+    unsigned e = __atomic_load_n(err_, __ATOMIC_ACQUIRE);
+    if (region_) e |= __atomic_load_n(&region_->header()->err, __ATOMIC_ACQUIRE);
+    return e;
+  }
+
+  void watchdog(Clock::time_point t0, bool timeout = true);
+
+  static void check_stream(hipStream_t s) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q != hipSuccess && q != hipErrorNotReady) fail(MPA_DEVICE_ERROR, "worker stream error: %s", hipGetErrorString(q));
+  }
+
+  void check_task(int64_t rank, const TaskSpec& ts, size_t sl, size_t rl);
+
+  void prepare_lsq(int64_t rank, const TaskSpec& ts);
+
+  // batched multi-iterate task: validate, size the residual scratch / partial slab
+  void prepare_lsqb(int64_t rank, const TaskSpec& ts);
+
+  // workgroups per task in a least-squares launch of `ntasks` tasks
+  int lsq_grid(const TaskSpec& ts, const HipWorker& w, int ntasks) const;
+
+  // Tasks of one flush (coordinator) or one doorbell scan (server).  Least-squares tasks
+  // without an injected delay run as ONE batched launch (per kernel variant, <=
+  // kMaxLsqTasks each) on an idle launch stream; a task with a delay runs on its worker's
+  // own stream behind a delay kernel, so a straggler never holds back another worker;
+  // reference-test tasks (kmap/echo) run per worker.  `staged`: the message sits in a
+  // mailbox and is first copied into the worker's device slot on the launch's stream.
+  void launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool on_coord = false);
+
+  // ---- straggler emulation -------------------------------------------------------------
+  // A worker with a delay schedule sleeps `delay` ns after its message is delivered and
+  // then computes (the reference worker's `sleep(rand())` before its reply,
+  // examples/iterative_example.jl:74).  The sleep is a host timer thread that launches the
+  // task kernel when it is due, so a sleeping worker holds no GPU queue: kernels parked
+  // in queues (a spinning delay kernel) made one straggler hold back another once the
+  // process had more streams than the GPU maps hardware queues for.
+  static uint64_t mono_ns() {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count());
+  }
+
+  struct Deferred {
+    uint64_t due;
+    std::function<void()> go;
+    bool operator<(const Deferred& o) const { return due > o.due; }  // min-heap on due
+  };
+
+  void defer(uint64_t due, std::function<void()> go);
+
+  void timer_loop();
+
+  // every deferred launch issued (shutdown)
+  void drain_deferred() {
+    std::unique_lock<std::mutex> lk(tmu_);
+    if (!timer_.joinable()) return;
+    tidle_.wait(lk, [this]() { return (deferred_.empty() && !tbusy_) || tstop_; });
+  }
+
+  // pending launches are dropped (the comm is being destroyed)
+  void stop_timer();
+
+  void check_timer();
+
+  void stage_in(const std::vector<int64_t>& ranks, hipStream_t s);
+
+  // MPA_DEBUG=1: pointer attributes of everything handed to a kernel
+  static void describe(const char* what, const void* p);
+
+  unsigned long long spin_ticks() const { return (unsigned long long)(timeout_s_ * rt_hz_); }
+
+  // the worker's own stream (delayed tasks, pre-armed tasks), created on first use
+  hipStream_t worker_stream(HipWorker& w) {
+    if (!w.stream) w.stream = make_queue_stream(dev_);
+    return w.stream;
+  }
+  // launch stream k (created on first use, up to kLaunchStreams)
+  hipStream_t launch_stream(size_t k) {
+    while (launch_streams_.size() <= k) launch_streams_.push_back(make_queue_stream(dev_));
+    return launch_streams_[k];
+  }
+
+  // a launch stream with no pending work (so a batch never queues behind an unrelated
+  // straggler's kernel); round-robin if every one is busy; a new one while fewer than
+  // kLaunchStreams exist and all are busy
+  hipStream_t pick_launch_stream();
+
+  void launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hipStream_t s);
+
+  // kernel arguments of one launch over `ranks`
+  // `share`: the launch grid is divided as if this many tasks ran at once (concurrent
+  // single-task launches of pre-armed workers)
+  LsqBatch build_lsq_batch(const std::vector<int64_t>& ranks, int dtype, double* bytes_out, int share = 0);
+
+  void launch_lsqb_batch(const std::vector<int64_t>& ranks, hipStream_t s) {
+    double bytes = 0;
+    const LsqbLaunch b = build_lsqb_batch(ranks, &bytes);
+    enqueue_lsqb(b, s, bytes);
+  }
+
+  // A batched multi-iterate launch: the single-pass kernel (lsqf_kernel.hip) where every
+  // task of the batch has the same slice count (cols <= 2048) and MPA_LSQF is not 0, else
+  // the two passes (lsqb_kernel.hip).
+  struct LsqbLaunch {
+    bool pair = false;   // lsqp (the default single pass)
+    bool pair8 = false;  // ... by the eight-wave cut (MPA_LSQP=8)
+    bool cpair = false;  // ... by column pairs (lsqc_kernel.hip)
+    bool fused = false;  // lsqf (opt-in)
+    bool quad = false;   // lsqq
+    LsqbBatch two{};
+    LsqfBatch one{};
+    LsqqBatch four{};
+    LsqpBatch halves{};
+    void set_go(const unsigned long long* go) {
+      if (pair) halves.t[0].go = go;
+      else if (quad) four.t[0].go = go;
+      else if (fused) one.t[0].go = go;
+      else two.t[0].go = go;
+    }
+  };
+
+  // the iterate-halves single pass (lsqp_kernel.hip): the default for cols <= 2048
+  // (MPA_LSQP=0 selects the two passes)
+  bool lsqp_enabled(const std::vector<int64_t>& ranks) const;
+
+  // column pairs (lsqc_kernel.hip): a row group of a task with more than 1024 columns is a
+  // pair of workgroups (one each, 1024 columns and all 64 iterates), of a narrower task one
+  // workgroup; 256 workgroups (one per CU) dealt over the tasks.  Row groups of at most
+  // kLsqcMaxBlocks blocks (the tag's block field), else the iterate-halves kernel stays.
+  static int lsqc_parts(int64_t cols) { return cols > kLsqcMemberCols ? 2 : 1; }
+  int lsqc_groups(const TaskSpec& ts, int split, int k) const;
+  bool lsqc_fits(const std::vector<int64_t>& ranks, const LsqpBatch& b, int share) const;
+  void build_lsqc(const std::vector<int64_t>& ranks, int share, LsqbLaunch& L);
+
+  // the iterate-quarter single pass (lsqq_kernel.hip): cols <= 2048 on every task
+  bool lsqq_enabled(const std::vector<int64_t>& ranks) const;
+
+  bool lsqf_enabled(const std::vector<int64_t>& ranks) const;
+
+  // kernel arguments over `ranks`; advances the workers' counter bases.  Algorithmic bytes
+  // per task: A + B + X + G.
+  // workers of this process with a batched least-squares task: a single-pass launch gives
+  // each of its tasks the grid share of one of them, so that the launches of one epoch (all
+  // fresh tasks, then a stale worker's re-dispatch, src/MPIAsyncPools.jl:177-184) run side
+  // by side on disjoint CUs instead of the later one queueing behind a full-chip grid
+  int lsqb_share() const;
+
+  LsqbLaunch build_lsqb_batch(const std::vector<int64_t>& ranks, double* bytes_out, int share = 0);
+
+  void enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int64_t armed_rank = 0);
+
+  // enqueue one least-squares launch on `s` (coordinator / server thread or timer thread)
+  void enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes, int64_t armed_rank = 0);
+
+ public:
+  // ---- kernel timing (HIP events around every least-squares launch) ----
+  void set_timing(bool on) {
+    if (!on) reap_timing(true);
+    timing_ = on;
+  }
+  // launches, total kernel ms, total algorithmic bytes, and the ms during which at least
+  // one timed launch was running (the union of their intervals: concurrent single-task
+  // launches of delayed workers overlap) since the last call
+  void timing(double out[4]);
+
+ private:
+  // epoch kernels timed since the last exchange_timing(): launches, ms, remote payload bytes
+  struct XTimed {
+    hipEvent_t start, stop;
+    double remote_bytes;
+  };
+  std::vector<XTimed> xtimed_;
+  double x_launches_ = 0, x_ms_ = 0, x_remote_ = 0;
+  void reap_xtiming();
+
+ public:
+  void exchange_timing(double out[3]);
+
+ private:
+  struct TimedLaunch {
+    hipEvent_t start, stop;
+    double bytes;
+    int64_t rank;  // pre-armed launch of this worker (0: none)
+    bool void_ = false;  // cancelled before it ran: not counted
+  };
+
+  // the pending timed launch armed for `rank` was cancelled
+  void void_timing(int64_t rank);
+
+  // caller holds tm_mu_ (event_pool_ is shared with the straggler timer thread)
+  hipEvent_t take_event();
+
+  void reap_timing(bool block);
+
+  Role role_ = SOLO;
+  std::vector<HipWorker> w_;
+  ShmRegion* region_ = nullptr;
+  int my_rank_ = 0;
+  int dev_ = 0;
+  hipStream_t coord_ = nullptr;
+  unsigned long long* flags_ = nullptr;
+  unsigned* err_ = nullptr;
+  unsigned* err_dev_ = nullptr;
+  unsigned long long* cancel_ = nullptr;  // server: cancel words of armed tasks (host-pinned)
+  bool xgmi_ = true;                      // MPA_XGMI=0: payloads always via the host mailbox
+  uint32_t* ctr_ = nullptr;
+  uint32_t* ticket_ = nullptr;
+  uint32_t ticket_count_ = 0;
+  // fused tail (maybe_ahead): the next least-squares launch carries tail_args_ (tail_next_);
+  // the epoch step of the next ahead epoch is already enqueued in a tail (tail_pending_)
+  uint32_t* tail_ctr_ = nullptr;
+  bool fused_tail_ = true;  // MPA_TAIL=0: a separate epoch kernel every epoch
+  // MPA_LSQP_SHARE=1: a single-pass launch's grid is dealt as if every local batched worker
+  // ran in it (off: batches share the coordinator stream, so a partial grid idles CUs; c5
+  // 19.9 vs 11.1 ms per epoch, profiles/r02_c5_lsqp_tuning.txt)
+  bool lsqp_share_ = false;
+  bool hold_ok_ = true;     // MPA_HOLD=0: a stale re-dispatch launches at once (flush_stale)
+  bool hold_next_ = false;  // set while flush_stale() flushes
+  bool may_hold_ = false;   // this call's wait completes without the held tasks (set_wait_hold)
+  std::vector<int64_t> held_;  // held re-dispatches, launched with the next batch
+  // held re-dispatches: held, later joined a batched launch, launched on their own
+  int64_t n_held_ = 0, n_held_joined_ = 0, n_held_alone_ = 0;
+  bool lsqp8_ = false;  // MPA_LSQP=8: the eight-wave single pass (lsqp_kernel.hip)
+  bool lsqc_ = false;   // MPA_LSQP=c: the column-pair single pass (lsqc_kernel.hip)
+  int lsqc_la_ = 2;     // MPA_LSQC_LA: its phase-1 lookahead in blocks (2; 1 for A/B)
+  // lsqp L2 prefetch lead in blocks (MPA_LSQP_PF; 0 = off; unset: 1 for lsqp4, 0 for the
+  // eight-wave cut).  lsqp4: 1 block 8.47 ms vs 9.50 without, 2-4 slower (L2 thrash);
+  // profiles/r02_c5_lsqp_tuning.txt
+  int lsqp_pfd_ = -1;
+  bool tail_next_ = false, tail_pending_ = false;
+  size_t tail_ranks_ = 0;
+  EpochArgs tail_args_{};
+  hipEvent_t xfer_ev_ = nullptr;
+  double rt_hz_ = 100e6;
+  double timeout_s_ = 600.0;
+  std::vector<int64_t> posts_;
+  std::vector<Harvest> harv_;
+  CallBufs b_;
+  std::vector<Harvest> call_posts_;  // (slot, rank) of every post() of the current call
+  bool defer_end_ = false;
+  bool has_update_ = false;
+  size_t harv_before_ = 0;  // harvests staged before the pending update
+  UpdateSpec upd_;
+  int64_t ahead_left_ = 0;
+  UpdateSpec ahead_pred_, ahead_upd_;
+  CallBufs ahead_bufs_;
+  bool ahead_update_ = false;
+  std::atomic<bool> timing_{false};  // read by the straggler timer thread's launches
+  bool debug_ = false;
+  int arm_mode_ = 0;
+  bool batch_gather_ = true;  // MPA_GATHER=0: a server launches whatever one doorbell scan found
+  // undelayed task batches run on the coordinator stream behind the exchange that delivered
+  // their messages (MPA_COORD_BATCH=0: on a launch stream behind a cross-queue event wait,
+  // which measured 75-200 us per hand-off on the k-of-n path, profiles/r01_c1_timeline.txt)
+  bool coord_batches_ = true;
+  std::vector<TimedLaunch> timed_;
+  std::vector<hipEvent_t> event_pool_;
+  int64_t t_launches_ = 0;
+  double t_ms_ = 0, t_bytes_ = 0;
+  std::vector<std::pair<double, double>> t_iv_;  // launch intervals (ms from anchor_)
+  hipEvent_t anchor_ = nullptr;
+  std::vector<hipStream_t> launch_streams_;
+  size_t next_launch_ = 0;
+  std::mutex tm_mu_;  // timed_ / event_pool_ (the timer thread also launches)
+  // straggler timer thread
+  std::thread timer_;
+  std::mutex tmu_;
+  std::condition_variable tcv_, tidle_;
+  std::vector<Deferred> deferred_;
+  bool tstop_ = false, tbusy_ = false;
+  std::atomic<bool> tfailed_{false};
+  std::mutex tfail_mu_;
+  std::string tfail_msg_;
+
+ public:
+  void init_ticket() {
+    ticket_ = ctr_ + kLsqCtrPerTask * nworkers_;
+    tail_ctr_ = ticket_ + 1;
+  }
+};
+
+}  // namespace mpa
