@@ -209,9 +209,14 @@ class HipComm final : public Comm {
 
   void begin_call(const CallBufs& b) override {
     if (role_ == SERVER) fail(MPA_ERROR, "asyncmap!/waitall! run on rank 0; this process serves workers (mpa_comm_serve)");
+    check_buffers(b);
     b_ = b;
     call_posts_.clear();
   }
+  // the call's buffers must be memory the GPU addresses (device memory, or host memory
+  // registered with HIP): pageable host memory -- a host array handed to a device comm by
+  // mistake -- is an ArgumentError, not a kernel fault.  Checked when the pointers change.
+  void check_buffers(const CallBufs& b);
 
   void post(int64_t i, int64_t rank, int64_t tag) override;
 
@@ -643,6 +648,7 @@ class HipComm final : public Comm {
   bool hold_ok_ = true;     // MPA_HOLD=0: a stale re-dispatch launches at once (flush_stale)
   bool hold_next_ = false;  // set while flush_stale() flushes
   bool may_hold_ = false;   // this call's wait completes without the held tasks (set_wait_hold)
+  const void* checked_bufs_[4] = {};  // the buffer pointers check_buffers() last accepted
   std::vector<int64_t> held_;  // held re-dispatches, launched with the next batch
   // held re-dispatches: held, later joined a batched launch, launched on their own
   int64_t n_held_ = 0, n_held_joined_ = 0, n_held_alone_ = 0;

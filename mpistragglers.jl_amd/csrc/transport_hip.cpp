@@ -182,6 +182,23 @@ HipComm::~HipComm() {
   delete region_;
 }
 
+void HipComm::check_buffers(const CallBufs& b) {
+  const void* ps[4] = {b.sl ? b.sendbuf : nullptr, b.rl ? b.recvbuf : nullptr, b.sl ? b.isendbuf : nullptr,
+                       b.rl ? b.irecvbuf : nullptr};
+  if (std::equal(ps, ps + 4, checked_bufs_)) return;
+  static const char* names[4] = {"sendbuf", "recvbuf", "isendbuf", "irecvbuf"};
+  for (int k = 0; k < 4; ++k) {
+    if (!ps[k]) continue;
+    hipPointerAttribute_t a{};
+    const hipError_t e = hipPointerGetAttributes(&a, ps[k]);
+    if (e != hipSuccess || a.type == hipMemoryTypeUnregistered) {
+      (void)hipGetLastError();
+      fail(MPA_ARGUMENT_ERROR, "%s is host memory the GPU cannot address: a device comm takes device buffers", names[k]);
+    }
+  }
+  std::copy(ps, ps + 4, checked_bufs_);
+}
+
 void HipComm::post(int64_t i, int64_t rank, int64_t tag) {
   (void)tag;
   if (shutdown_) fail(MPA_ERROR, "comm has been shut down");

@@ -74,3 +74,29 @@ def test_julia_capi_types_match_arity():
         assert m, name
         types = [t for t in m.group(1).split(", ") if t.strip(",")]
         assert len(types) == len(params), (name, types)
+
+
+def test_julia_mpi_extension_matches_its_header():
+    """The package extension for MPI.Comm ccalls mpa_comm_create_mpi as
+    include/mpiasyncpools_mpi.h declares it (int64_t Fortran handle, mpa_comm** out)."""
+    from mpiasyncpools import abi
+    decl = {n: (r, p) for n, r, p in abi.parse(open(os.path.join(ROOT, "include", "mpiasyncpools_mpi.h")).read())}
+    assert "mpa_comm_create_mpi" in decl
+    ret, params = decl["mpa_comm_create_mpi"]
+    src = open(os.path.join(ROOT, "julia", "MPIAsyncPoolsHIP", "ext", "MPIAsyncPoolsHIPMPIExt.jl")).read()
+    m = re.search(r"ccall\(\(:mpa_comm_create_mpi, libmpi_t\), (\w+), \(([^)]*)\)", src)
+    assert m, "the extension ccalls mpa_comm_create_mpi"
+    assert m.group(1) == abi.julia_type(ret)
+    assert [t.strip() for t in m.group(2).split(",")] == [abi.julia_type(t) for t, _ in params]
+    proj = open(os.path.join(ROOT, "julia", "MPIAsyncPoolsHIP", "Project.toml")).read()
+    assert 'MPIAsyncPoolsHIPMPIExt = "MPI"' in proj
+
+
+def test_julia_byte_counts_are_data_bytes():
+    """Buffer byte counts handed to the ABI are length * element size (`_nbytes`), never
+    `sizeof(buffer)`, which for a wrapper array type is the wrapper's size."""
+    src = open(os.path.join(JL, "MPIAsyncPoolsHIP.jl")).read()
+    for name in ("mpa_asyncmap", "mpa_waitall", "mpa_lsq_descent", "mpa_lsqb_descent"):
+        for args in _calls(src, name):
+            assert not any(re.search(r"\bsizeof\(", a) for a in args), (name, args)
+    assert "DistComm" in src and "serve!" in src and "set_task_lsq_batch!" in src and "lsqb_descent!" in src

@@ -375,3 +375,25 @@ def test_read_bandwidth_probe(M, torch_mod):
         assert 500.0 < gbps < 9000.0, (grid, gbps)
     with pytest.raises(M.ArgumentError):
         M.read_bandwidth(buf, grid=0)
+
+
+def test_host_buffers_refused_by_a_device_comm(M, torch_mod):
+    """Pageable host memory handed to a device comm is an ArgumentError naming the buffer
+    (a Julia user passing a host Vector), not a kernel reading host addresses; device buffers
+    keep working on the same pool afterwards."""
+    torch = torch_mod
+    comm = M.DeviceComm(2)
+    for r in (1, 2):
+        comm.set_task(r, "kmap2")
+    pool = M.MPIAsyncPool(2)
+    host = np.zeros(6)
+    with pytest.raises(M.ArgumentError, match="recvbuf is host memory"):
+        M.asyncmap_(pool, torch.zeros(1, dtype=torch.float64, device="cuda"), host,
+                    torch.zeros(2, dtype=torch.float64, device="cuda"), torch.zeros(6, dtype=torch.float64, device="cuda"),
+                    comm, nwait=2)
+    assert not pool.active.any()  # refused before any state change
+    s = torch.full((1,), 5.0, dtype=torch.float64, device="cuda")
+    rb = torch.zeros(6, dtype=torch.float64, device="cuda")
+    M.asyncmap_(pool, s, rb, torch.zeros(2, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), comm, nwait=2)
+    assert rb.cpu().tolist() == [1, 1, 5, 2, 1, 5]
+    comm.close()
