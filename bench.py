@@ -111,6 +111,35 @@ def cpu_baseline(cfg, seconds):
                       f"machine); {r['alg_GBps']:.1f} GB/s algorithmic"}
 
 
+def mpi_baseline(cfg, seconds):
+    """oracle/_build/mpi_lsq_baseline (kind "mpi"): BASELINE configs[0] as the reference runs
+    it, the restated coordinator (src/MPIAsyncPools.jl over MPI's own verbs) and one worker
+    PROCESS per worker computing its fp64 shard gradient, under MPICH's mpiexec."""
+    exe = os.path.join(ROOT, "oracle", "_build", "mpi_lsq_baseline")
+    mpi_dir = os.environ.get("MPI_DIR", "/opt/conda")
+    mpiexec = os.path.join(mpi_dir, "bin", "mpiexec")
+    if not os.path.exists(exe) and os.path.exists(os.path.join(mpi_dir, "include", "mpi.h")):
+        try:
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "mpi", f"MPI_DIR={mpi_dir}"])
+        except Exception as e:
+            return {"value": None, "unit": "iterations/s", "error": f"build failed: {e}"[:200]}
+    if not (os.path.exists(exe) and os.path.exists(mpiexec)):
+        return {"value": None, "unit": "iterations/s", "error": "MPICH (mpiexec, mpi.h) not present on this host"}
+    cmd = [mpiexec, "-n", str(cfg["workers"] + 1), exe, "--rows", str(cfg["rows"]), "--cols", str(cfg["cols"]),
+           "--nwait", str(cfg["nwait"]), "--seconds", str(int(seconds))]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds * 4 + 120, check=True).stdout
+        r = json.loads(out.strip().splitlines()[-1])
+    except Exception as e:  # report, never fake
+        return {"value": None, "unit": "iterations/s", "error": str(e)[:200]}
+    host_cores, host_model = host_cpu()
+    return {"value": round(r["it_per_s"], 4), "unit": "iterations/s", "cores": r["processes"], "kind": "mpi",
+            "processes": r["processes"], "host_cores": host_cores, "host_cpu_model": host_model,
+            "sample": f"{r['epochs']} epochs in {r['seconds']:.1f} s of the full {cfg['config']} problem: 1 coordinator "
+                      f"+ {r['workers']} worker processes over MPICH (mpiexec), the restated asyncmap! with MPI's own "
+                      f"verbs, fp64 shard gradients, nwait={r['nwait']}"}
+
+
 def step_size(rows, cols):
     """0.9 / L with L ~ ||A||^2 for U(-1,1)/sqrt(cols) entries."""
     L = rows / (3.0 * cols) * (1.0 + np.sqrt(cols / rows)) ** 2
@@ -427,7 +456,13 @@ def run_single(args, cfg):
                   "fresh_at_last_epoch": fresh})
     if cfg["config"] == "c2":
         extra["loop"] += "; python loop beside it"
-    extra["cpu_baseline"] = None if (args.no_cpu_baseline or cfg["config"] != "c2") else cpu_baseline(cfg, args.cpu_seconds)
+    # the CPU beside the device: c2 threaded (the bench's headline config), c1 as the reference
+    # runs configs[0] (coordinator + worker processes over MPI)
+    extra["cpu_baseline"] = None
+    if not args.no_cpu_baseline and cfg["config"] == "c2":
+        extra["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    elif not args.no_cpu_baseline and cfg["config"] == "c1":
+        extra["cpu_baseline"] = mpi_baseline(cfg, args.cpu_seconds)
     print(json.dumps(report(args, cfg, 1, el, [timing], extra)), flush=True)
     comm.shutdown()
     comm.close()

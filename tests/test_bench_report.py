@@ -126,3 +126,18 @@ def test_trace_window_skips_launches_after_the_timed_region(tmp_path):
     w = json.loads(out.read_text())
     assert w["launches"] == 4 and w["launches_after_timed"] == 1
     assert abs(w["avg_ms"] - (8.5 + 8.4 + 8.4 + 8.6) / 4) < 1e-9
+
+
+def test_c1_mpi_cpu_baseline_runs():
+    """bench.py's c1 CPU baseline (kind "mpi"): the restated coordinator and 3 worker
+    processes over MPICH run the configs[0] descent and report their rate and cores."""
+    import importlib.util
+    if not os.path.exists("/opt/conda/bin/mpiexec"):
+        pytest.skip("MPICH not present")
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    cfg = dict(b.CONFIGS["c1"], config="c1")
+    r = b.mpi_baseline(cfg, 1)
+    assert r["kind"] == "mpi" and r["value"] > 100 and r["processes"] == 4 and r["cores"] == 4, r
+    assert "3 worker processes over MPICH" in r["sample"]
