@@ -49,5 +49,37 @@ __device__ __forceinline__ bool disarmed(const unsigned long long* go, unsigned 
   return ((unsigned long long)hi << 32 | lo) == seq;
 }
 
+// A device-armed task of a worker process is launched before rank 0 posts
+// it and waits in-kernel for its doorbell: a word in this GPU's fine-grained message slot
+// that rank 0's exchange / epoch kernel stores over xGMI after the message (release, system
+// scope).  Thread 0 of every workgroup polls it with relaxed system-scope loads (they bypass
+// the caches and invalidate nothing: an acquiring poll invalidated L2 at every load and, on a
+// GPU shared with rank 0 in a one-GPU rehearsal, slowed its kernels 1.8x) until it reaches the
+// task's seq, with or without kCancelBit (a task its server cancelled runs and then neither
+// writes nor publishes, as its go word says), then acquires once: the message the store
+// released is visible to the workgroup after the barrier.  Bounded by spin_ticks: error bit
+// 64 and no work.  Call with the whole workgroup.
+__device__ __forceinline__ bool wait_door(const unsigned long long* door, unsigned long long seq,
+                                          unsigned long long spin_ticks, unsigned* err) {
+  __shared__ int s_door_ok;
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = rt_now();
+    int ok = 1;
+    for (unsigned k = 0;
+         (__hip_atomic_load(door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & ~kCancelBit) < seq; ++k) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((k & 255) == 255 && rt_now() - t0 > spin_ticks) {
+        __hip_atomic_fetch_or(err, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once
+    s_door_ok = ok;
+  }
+  __syncthreads();
+  return s_door_ok != 0;
+}
+
 }  // namespace dev
 }  // namespace mpa

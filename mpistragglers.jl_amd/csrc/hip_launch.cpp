@@ -350,6 +350,11 @@ void HipComm::launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hip
       fail(MPA_ERROR, "fused tail: the launch does not cover the epoch's %zu workers", tail_ranks_);
     b.tail = epoch_vec(dtype, tail_args_) ? 2 : 1;
     b.tail_ctr = tail_ctr_;
+    b.tail_nwait = tail_nwait_;
+    for (int k = 0; k < tail_nwait_; ++k) {
+      b.tail_word[k] = tail_word_[k];
+      b.tail_target[k] = tail_target_[k];
+    }
     b.ep = tail_args_;
     tail_next_ = false;
   }
@@ -499,6 +504,8 @@ HipComm::LsqbLaunch HipComm::build_lsqb_batch(const std::vector<int64_t>& ranks,
     L.pair8 = lsqp8_;
     LsqpBatch& b = L.halves;
     b.ntasks = int(ranks.size());
+    b.err = err_dev_;  // the device-armed doorbell wait's error word and bound
+    b.spin_ticks = spin_ticks();
     b.pfd = lsqp_pfd_ >= 0 ? lsqp_pfd_ : (lsqp8_ ? 0 : 1);
     { const char* d = measure_env("MPA_LSQP_DBG"); b.dbg = d ? std::atoi(d) : 0; }
     // one workgroup per CU: 128 pairs (256 workgroups), dealt evenly over max(tasks,

@@ -94,9 +94,14 @@ void HipComm::serve() {
   }
 }
 
+// Device-armed tasks: least-squares workers without injected delays whose
+// messages arrive in this GPU's slot (device payload path).  MPA_ARM: 0 never, 1 every such
+// worker, 2 (default) where the process serves one worker (the N = 8 placement; a process
+// with several workers launches the tasks of a flush as one batch instead).
 bool HipComm::armable(int64_t rank) const {
   const TaskSpec& ts = tasks_[size_t(rank - 1)];
-  if (arm_mode_ == 0 || !((ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty()))
+  const HipWorker& w = w_[size_t(rank - 1)];
+  if (arm_mode_ == 0 || !w.path_dev || !((ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty()))
     return false;
   if (arm_mode_ == 1) return true;
   int here = 0;
@@ -104,6 +109,10 @@ bool HipComm::armable(int64_t rank) const {
   return here == 1;
 }
 
+// The worker's next task is launched before rank 0 posts it: every workgroup waits in-kernel
+// for the worker's device doorbell (wait_door), which rank 0's exchange / epoch kernel stores
+// over xGMI right after the message, so ring -> start is a poll of this GPU's memory instead
+// of the serve loop's host poll and a launch (19 us of the traced c2 N = 2 epoch).
 void HipComm::arm(int64_t rank) {
   HipWorker& w = w_[size_t(rank - 1)];
   const TaskSpec& ts = tasks_[size_t(rank - 1)];
@@ -112,26 +121,22 @@ void HipComm::arm(int64_t rank) {
   w.arm_tbase = w.lsqb_tbase;
   w.arm_fsbase = w.lsqf_sbase;
   w.arm_ftbase = w.lsqf_tbase;
-  HIPCHECK(hipStreamWaitValue64(worker_stream(w), w.box_door_dev, s, hipStreamWaitValueGte, ~0ull));
   w.seq = s;
   w.sl = task_msg_bytes(ts);
   w.rl = w.sl * (ts.kind == MPA_TASK_LSQ_BATCH ? 2 : 1);
   w.x = w.xslot;
   w.out = reply_dst(w);
-  if (!w.path_dev) {  // host mailbox: stage the message into the device slot first
-    ExchangeBuilder xb(ticket_, &ticket_count_, w.stream);
-    xb.copy(w.box_msg_dev, w.xslot, w.sl);
-    xb.launch();
-  }
   double bytes = 0;
   if (ts.kind == MPA_TASK_LSQ) {
     LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes, armed_share());
     b.t[0].go = w.cancel_dev;
-    enqueue_lsq(b, ts.dtype, int(ts.cols), w.stream, bytes, rank);
+    b.t[0].door = own_door(w);
+    enqueue_lsq(b, ts.dtype, int(ts.cols), worker_stream(w), bytes, rank);
   } else {
     LsqbLaunch b = build_lsqb_batch({rank}, &bytes, armed_share());
     b.set_go(w.cancel_dev);
-    enqueue_lsqb(b, w.stream, bytes, rank);
+    b.set_door(own_door(w));
+    enqueue_lsqb(b, worker_stream(w), bytes, rank);
   }
   w.armed = true;
 }
@@ -141,18 +146,16 @@ void HipComm::disarm_all() {
   for (int64_t r = 1; r <= nworkers_; ++r) {
     HipWorker& w = w_[size_t(r - 1)];
     if (!w.here || !w.armed) continue;
-    unsigned long long expect = w.seq - 1;
+    // release the waiting task with the cancel bit unless rank 0 rang meanwhile (its kernel
+    // stores the device word after the shm one): cancel word first, so every workgroup of a
+    // released task finds it; a cancelled task runs but neither writes nor publishes
     bool cancelled = false;
     if (__atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE) < w.seq) {
       __atomic_store_n(w.cancel_host, w.seq, __ATOMIC_SEQ_CST);
-      cancelled = __atomic_compare_exchange_n(&w.box->doorbell, &expect, w.seq | kCancelBit, false, __ATOMIC_SEQ_CST,
-                                              __ATOMIC_SEQ_CST);
+      cancelled = door_cas(w, w.seq - 1, w.seq | kCancelBit);
     }
     (void)hipStreamSynchronize(w.stream);
-    if (cancelled) {
-      unsigned long long c2 = w.seq | kCancelBit;  // restore unless rank 0 rang meanwhile
-      __atomic_compare_exchange_n(&w.box->doorbell, &c2, w.seq - 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
-    }
+    if (cancelled) (void)door_cas(w, w.seq | kCancelBit, w.seq - 1);  // back to "not rung"
     __atomic_store_n(w.cancel_host, 0ull, __ATOMIC_SEQ_CST);
     if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) {  // it did not run
       w.seq -= 1;
@@ -164,6 +167,16 @@ void HipComm::disarm_all() {
     }
     w.armed = false;
   }
+}
+
+// the worker's device doorbell := desired if it holds expect (a kernel on a launch stream:
+// the word is this GPU's fine-grained memory, which rank 0 stores over xGMI); true if it did
+bool HipComm::door_cas(const HipWorker& w, unsigned long long expect, unsigned long long desired) {
+  hipStream_t s = launch_stream(0);
+  __atomic_store_n(&cancel_[nworkers_], ~0ull, __ATOMIC_SEQ_CST);  // scratch: the word's old value
+  HIPCHECK(launch_door_cas(own_door(w), expect, desired, &cancel_[nworkers_], s));
+  HIPCHECK(hipStreamSynchronize(s));
+  return __atomic_load_n(&cancel_[nworkers_], __ATOMIC_ACQUIRE) == expect;
 }
 
 void* HipComm::ipc_alloc(size_t bytes, char* handle, volatile uint32_t* state) {

@@ -300,27 +300,24 @@ class HipComm final : public Comm {
   void on_task_changed(int64_t rank) override;
 
   // ---- worker process: watch the doorbells of the workers served here ----
-  // Least-squares workers without a delay schedule are PRE-ARMED: their next task is
-  // already queued on the worker's own stream behind hipStreamWaitValue64 on the mailbox
-  // doorbell, so the GPU starts it when rank 0's exchange kernel rings (3.2 us ring -> task
-  // start, against 13.4 us for host polling + launch; profiles/r01_probe_waitvalue.txt).
-  // Other workers (the reference's test programs, injected delays) are launched by this
-  // thread when it sees their doorbell.  serve() returns at pause / shutdown after
-  // disarming: the pending waits are released with kCancelBit and their tasks return
-  // without computing or publishing.
+  // Least-squares workers without a delay schedule whose messages arrive in this GPU's slot
+  // are DEVICE-ARMED (armable): their next task is already launched and waits in-kernel for
+  // the worker's device doorbell, which rank 0 stores over xGMI right after the message.
+  // Other workers (the reference's test programs, injected delays, the host mailbox) are
+  // launched by this thread when it sees their shared-memory doorbell.  serve() returns at
+  // pause / shutdown after disarming: waiting tasks are released with kCancelBit and return
+  // without writing or publishing.
   void serve();
 
-  // ---- pre-armed tasks (server) ----
-  // Off by default (MPA_ARM=2: where a process serves ONE worker; MPA_ARM=1: every eligible
-  // worker).  The armed launch saves the host's doorbell poll + launch (3.2 vs 13.4 us ring ->
-  // start) but its task ran 7-15x longer than the same task launched by the host: every
-  // workgroup reads the host-memory go word before it starts (one-GPU N = 2 rehearsal, c1:
-  // 134 us with every lane reading, 73 us with one lane per wave, 9.6 us host-launched;
-  // 106 vs 48 us per epoch; c2 with 4 armed workers 1.20 vs 0.74 ms; profiles/r02_arm_go_word.txt).
-  // With several workers the host-launched path also batches them into one launch
-  // (profiles/r01_n2_arm_ab.txt).
+  // ---- device-armed tasks (server) ----
+  // MPA_ARM=2 (default): where a process serves ONE worker (N = 8); MPA_ARM=1: every eligible
+  // worker; MPA_ARM=0: never.  Round 2's armed launch waited behind hipStreamWaitValue64 on
+  // the host doorbell (a blit kernel per wait) and read the host go word from every lane:
+  // 7-15x slower tasks (profiles/r02_arm_go_word.txt); the go word is now read once by the
+  // reply's writer and the wait is the kernel's own poll of device memory (wait_door).  With
+  // several workers the host-launched path batches a flush's tasks into one launch.
   bool armable(int64_t rank) const;
-  // local workers that serve() pre-arms: each armed launch gets its share of the launch grid
+  // local workers that serve() arms: each armed launch gets its share of the launch grid
   int armed_share() const {
     int k = 0;
     for (int64_t r = 1; r <= nworkers_; ++r) k += w_[size_t(r - 1)].here && armable(r);
@@ -333,16 +330,16 @@ class HipComm final : public Comm {
                                          : size_t(ts.cols) * (ts.dtype == MPA_F64 ? 8 : 4);
   }
 
-  // queue task seq+1 of `rank` on its stream: wait for the doorbell, stage the message and
-  // the doorbell value (the task's go word), run the task
+  // launch task seq+1 of `rank` on its stream, waiting in-kernel for the device doorbell
   void arm(int64_t rank);
 
-  // release every pending armed wait: a task whose doorbell rank 0 has not rung is
-  // cancelled (cancel word := its seq, then doorbell := seq | kCancelBit to release the
-  // wait; both restored once the stream has drained), one already rung completes.  A task
-  // cancelled in a race with rank 0's ring did not run: its doorbell is served by the next
-  // serve() session (seq rolled back).
+  // release every waiting armed task: one whose doorbell rank 0 has not rung is cancelled
+  // (cancel word := its seq, then device doorbell := seq | kCancelBit to release the wait;
+  // both restored once the stream has drained), one already rung completes.  A task
+  // cancelled in a race with rank 0's ring did not publish: its doorbell is served by the
+  // next serve() session (seq rolled back).
   void disarm_all();
+  bool door_cas(const HipWorker& w, unsigned long long expect, unsigned long long desired);
 
   void pause_servers() {
     if (role_ != COORD) fail(MPA_ERROR, "only rank 0 of a multi-process communicator pauses its servers");
@@ -407,6 +404,15 @@ class HipComm final : public Comm {
   const uint8_t* reply_src(const HipWorker& w) const { return w.path_dev ? w.reply_inbox : w.box_reply_dev; }
   // where a served worker's task writes its reply
   uint8_t* reply_dst(const HipWorker& w) const { return w.path_dev ? w.peer_reply : w.box_reply_dev; }
+  // the worker's device doorbell word, after the message in its fine-grained slot (server:
+  // its own slot; rank 0: the slot opened by IPC, device path only)
+  size_t door_off() const { return (region_->max_msg() + 255) / 256 * 256; }
+  unsigned long long* peer_door(const HipWorker& w) const {
+    return reinterpret_cast<unsigned long long*>(w.peer_msg + door_off());
+  }
+  unsigned long long* own_door(const HipWorker& w) const {
+    return reinterpret_cast<unsigned long long*>(w.xslot + door_off());
+  }
 
   bool done(int64_t rank) const {
     const HipWorker& w = w_[size_t(rank - 1)];
@@ -548,6 +554,12 @@ class HipComm final : public Comm {
       else if (fused) one.t[0].go = go;
       else two.t[0].go = go;
     }
+    // device-armed launches: the product's kernels (lsqp4, the two passes) only
+    void set_door(const unsigned long long* door) {
+      if (pair && !pair8 && !cpair) halves.t[0].door = door;
+      else if (!pair && !quad && !fused) two.t[0].door = door;
+      else fail(MPA_ERROR, "device-armed tasks run the product's batched kernels only");
+    }
   };
 
   // the iterate-halves single pass (lsqp_kernel.hip): the default for cols <= 2048
@@ -660,8 +672,12 @@ class HipComm final : public Comm {
   // profiles/r02_c5_lsqp_tuning.txt
   int lsqp_pfd_ = -1;
   bool tail_next_ = false, tail_pending_ = false;
-  size_t tail_ranks_ = 0;
+  size_t tail_ranks_ = 0;  // local tasks of the launch that carries the tail
   EpochArgs tail_args_{};
+  // rank 0: the completion words of the epoch's remote workers the tail waits for
+  int tail_nwait_ = 0;
+  const unsigned long long* tail_word_[kMaxEpochChunks] = {};
+  unsigned long long tail_target_[kMaxEpochChunks] = {};
   hipEvent_t xfer_ev_ = nullptr;
   double rt_hz_ = 100e6;
   double timeout_s_ = 600.0;

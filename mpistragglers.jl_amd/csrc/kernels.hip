@@ -238,6 +238,20 @@ hipError_t launch_exchange(const ExchangeArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(64) door_cas_kernel(unsigned long long* door, unsigned long long expect,
+                                                      unsigned long long desired, unsigned long long* old_out) {
+  if (threadIdx.x != 0) return;
+  unsigned long long e = expect;
+  __hip_atomic_compare_exchange_strong(door, &e, desired, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(old_out, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_door_cas(unsigned long long* door, unsigned long long expect, unsigned long long desired,
+                           unsigned long long* old_out, hipStream_t s) {
+  hipLaunchKernelGGL(door_cas_kernel, dim3(1), dim3(64), 0, s, door, expect, desired, old_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_kmap(const KmapArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(kmap_task_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();

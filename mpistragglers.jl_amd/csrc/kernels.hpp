@@ -100,6 +100,10 @@ struct LsqTask {
   // to seq means "disarmed", and the task returns without computing or publishing (NULL:
   // not armed)
   const unsigned long long* go;
+  // device-armed launch of a worker process: the worker's doorbell word in this GPU's
+  // message slot, which rank 0 rings over xGMI; every workgroup waits for it to reach seq
+  // before any work (wait_door, device_common.hpp).  NULL: launched when rung
+  const unsigned long long* door;
   // wide rows (cols > 2048, lsqw_kernel.hip): the residual r = A x - b (rows T), the
   // per-slice tree and slice-completion counters, and the row groups of the second pass
   void* r;
@@ -131,12 +135,20 @@ struct LsqBatch {
   // Fused tail (the native descent loop at integer nwait == n): the task of
   // this launch that completes LAST runs the NEXT epoch's coordinator step `ep` (harvest
   // copies of this launch's replies, the iterate update, the dispatch copies of the next
-  // launch's messages; local workers only, no doorbells) in its last workgroup, so the
-  // descent loop's epoch is one launch.  tail: 0 none, 1 scalar elements, 2 16-B vectors.
+  // launch's messages) in its last workgroup, so the descent loop's epoch is one launch.
+  // tail: 0 none, 1 scalar elements, 2 16-B vectors.  On rank 0 of a multi-process comm the
+  // epoch also has workers served by other processes: the tail first waits for their
+  // completion words (tail_word[k] >= tail_target[k], bounded: err bit 32), harvests their
+  // replies from its inboxes, writes their next messages over xGMI and rings their doorbells
+  // (ep.door), in place of wait_words_kernel + epoch_kernel.
   int tail;
   uint32_t* tail_ctr;  // task completions of this launch (the last one resets it)
+  int tail_nwait;
+  const unsigned long long* tail_word[kMaxEpochChunks];
+  unsigned long long tail_target[kMaxEpochChunks];
   EpochArgs ep;
 };
+static_assert(sizeof(LsqBatch) <= 4096, "LsqBatch is passed by value as kernel arguments (4 KiB)");
 // Returns hipErrorInvalidValue if no kernel variant covers (dtype, cols).  cols > 2048 runs
 // the wide two passes (launch_lsqw).
 hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s);
@@ -170,6 +182,7 @@ struct LsqbTask {
   int nrange, nslice;  // pass-2 grid = nrange * nslice
   uint32_t sbase, tbase;  // ctr values before this launch (every slice counter moves alike)
   const unsigned long long* go;  // as LsqTask::go
+  const unsigned long long* door;  // as LsqTask::door
 };
 struct LsqbBatch {
   int ntasks;
@@ -203,6 +216,7 @@ struct LsqpTask {
   int64_t rows, lda;
   int cols;
   const unsigned long long* go;  // as LsqTask::go
+  const unsigned long long* door;  // as LsqTask::door
   // column pairs (lsqc_kernel.hip) only
   unsigned long long* xg;  // [kLsqpMaxGroups][2][kLsqcXR][4][64][4] {tag, fp32} exchange granules
   int parts;               // members per row group: 2 if cols > kLsqcMemberCols, else 1
@@ -215,6 +229,7 @@ struct LsqpBatch {
   LsqpTask t[kMaxLsqTasks];
   // column pairs (lsqc_kernel.hip) only
   uint32_t* tick;  // workgroup ticket counter (zero between launches: the last taker resets it)
+  // bounded in-kernel waits (lsqc's exchange, a device-armed task's doorbell): error word, bound
   unsigned* err;
   unsigned long long spin_ticks;
 };
@@ -301,6 +316,11 @@ struct KmapArgs {
   Publish pub;
 };
 hipError_t launch_kmap(const KmapArgs& a, hipStream_t s);
+// a worker process moves its device doorbell word (a device-armed task's cancel / restore,
+// hip_server.cpp disarm_all): *door = desired if it holds expect; the value it held goes to
+// *old_out (host-pinned)
+hipError_t launch_door_cas(unsigned long long* door, unsigned long long expect, unsigned long long desired,
+                           unsigned long long* old_out, hipStream_t s);
 
 
 constexpr int kMaxAggregate = 256;

@@ -123,6 +123,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   while (ti + 1 < batch.ntasks && int(blockIdx.x) >= batch.block0[ti + 1]) ++ti;
   const LsqTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block0[ti];
+  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed
   // A pre-armed task its server cancelled (the host-memory go word holds its seq) computes
   // but neither writes its reply nor publishes.  The word is read ONCE, by the workgroup that
   // writes the reply, at that point: every lane of every workgroup reading it before any work
@@ -318,9 +319,43 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   }
   __syncthreads();
   if (!s_ticket) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (batch.tail_nwait > 0) {
+    // the workers served by other processes: wave 0 polls their completion words (lane k:
+    // word k, relaxed system-scope loads of the shared mailbox), as wait_words_kernel does
+    if (tid < 64) {
+      const int k = tid;
+      bool ok = k >= batch.tail_nwait;
+      const unsigned long long t0 = rt_now();
+      for (unsigned it = 0;; ++it) {
+        if (!ok) ok = __hip_atomic_load(batch.tail_word[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= batch.tail_target[k];
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
+        __builtin_amdgcn_s_sleep(2);
+        if ((it & 63) == 63 && rt_now() - t0 > batch.spin_ticks) {
+          if (k == 0) __hip_atomic_fetch_or(batch.err, 32u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          s_ticket = 0;  // no step: the host watchdog reports the error word
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (!s_ticket) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the replies the remote tasks released
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
   if (batch.tail == 2) epoch_elems<T, E>(batch.ep, tid, kThreads);
   else epoch_elems<T, 1>(batch.ep, tid, kThreads);
+  if (batch.ep.ndoor == 0) return;
+  // the next messages of remote workers are in their slots: release them at system scope,
+  // then ring the doorbells (as epoch_kernel's last block)
+  drain_vm();
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence_system();
+    drain_vm();
+    for (int d = 0; d < batch.ep.ndoor; ++d)
+      __hip_atomic_store(batch.ep.door[d], batch.ep.doorval[d], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 template <typename T, int VPL, int RB, int MODE>

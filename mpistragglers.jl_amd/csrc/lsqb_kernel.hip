@@ -93,6 +93,7 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_chunked_kernel(LsqbBatc
   const int ti = task_of(batch.block1, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block1[ti];
+  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed (pass 2 follows on the stream)
   if (disarmed(a.go, a.seq)) return;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -250,6 +251,7 @@ __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch)
   const int ti = task_of(batch.block1, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block1[ti];
+  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed (pass 2 follows on the stream)
   if (disarmed(a.go, a.seq)) return;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -105,18 +105,24 @@ __device__ __forceinline__ void vm_wait() {
 // it (the kernel counts its DMAs itself, vm_wait above)
 __device__ __forceinline__ void dma1k(const void* sbase, uint32_t voff, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l) : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(l) : "memory");
 }
 __device__ __forceinline__ void dma16(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(l) : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
 }
 
 // 16-B chunk c of a 512-B sub-slice row r sits at chunk position c ^ swz(r) (bits 1-3 only:
 // conflict-free row reads in phase 1 and transposed reads in phase 2, as in lsqp4)
 __device__ __forceinline__ void dma16_sc1(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(src), "s"(l) : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
 }
 
 __host__ __device__ constexpr int swz(int r) { return 2 * (r & 3) + (r & 8); }

@@ -95,16 +95,21 @@ __device__ __forceinline__ void barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n
 // block too; the kernel orders its reads itself (vmcnt per block).
 __device__ __forceinline__ void dma_row(const void* sbase, uint32_t voff, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l)
-               : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(l) : "memory");
 }
 __device__ __forceinline__ void pf4(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(l) : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
 }
 __device__ __forceinline__ void dma16(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(l) : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
 }
 
 // 16-B chunk c of strip row r sits at chunk position c ^ sw(r) (bits 1-2 only: chunk pairs
@@ -151,6 +156,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   // every workgroup before any work (profiles/r02_arm_go_word.txt)
   const int q = pidx - batch.grp0[ti];
   const int ng = batch.grp0[ti + 1] - batch.grp0[ti];
+  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed
 
   const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
   const int qq = (lane >> 2) & 3, p4 = lane & 3;

@@ -85,7 +85,9 @@ __device__ __forceinline__ void barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n
 // each wave reads only what it loaded, or what crossed a barrier after the loader's wait).
 __device__ __forceinline__ void dma16(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(l) : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
 }
 
 // L2 prefetch of 4 B per lane into a per-wave sink nobody reads (global_load_lds_dword): a
@@ -95,7 +97,9 @@ __device__ __forceinline__ void dma16(const void* src, void* lds) {
 // KiB in flight per CU to hide an HBM miss; the ring gives one to two slots per wave)
 __device__ __forceinline__ void pf4(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(l) : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
 }
 
 // 16-B chunk c (8 columns) of slice row r is stored at chunk position c ^ swz(r): distinct

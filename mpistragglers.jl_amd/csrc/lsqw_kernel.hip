@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(kThreads) lsqw_resid_kernel(LsqBatch batch) {
   while (ti + 1 < batch.ntasks && int(blockIdx.x) >= batch.block0[ti + 1]) ++ti;
   const LsqTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block0[ti];
+  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed (pass 2 follows on the stream)
   if (disarmed(a.go, a.seq)) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);

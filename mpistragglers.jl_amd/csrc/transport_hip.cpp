@@ -76,7 +76,9 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
       w.flag_host = &w.box->done;
       w.flag_dev = region_->dev(&w.box->done);
       w.box->server_dev = dev_;
-      w.xslot = static_cast<uint8_t*>(ipc_alloc(region_->max_msg(), w.box->msg_handle, &w.box->msg_ipc));
+      // the message slot, then the worker's device doorbell word (device-armed tasks wait on it)
+      w.xslot = static_cast<uint8_t*>(ipc_alloc(door_off() + 256, w.box->msg_handle, &w.box->msg_ipc));
+      HIPCHECK(hipMemset(w.xslot + door_off(), 0, 256));
       w.cancel_host = &cancel_[r - 1];
       w.cancel_dev = &cancel_[r - 1];
     } else if (w.remote) {
@@ -111,9 +113,10 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   rt_hz_ = khz > 0 ? double(khz) * 1e3 : 100e6;
   const char* t = std::getenv("MPA_WAIT_TIMEOUT_S");
   timeout_s_ = t ? std::atof(t) : 600.0;
-  // unset / 0: never pre-arm; 1: arm every eligible worker; 2: when a process serves one
+  // device-armed server tasks (hip_server.cpp): 0 never, 1 every eligible worker, 2 (default)
+  // where a process serves one worker
   const char* arm = std::getenv("MPA_ARM");
-  arm_mode_ = arm && *arm == '1' ? 1 : arm && *arm == '2' ? 2 : 0;
+  arm_mode_ = arm && *arm == '0' ? 0 : arm && *arm == '1' ? 1 : 2;
   const char* cb = measure_env("MPA_COORD_BATCH");
   coord_batches_ = !(cb && *cb == '0');
   fused_tail_ = !env_off("MPA_TAIL");
@@ -293,10 +296,11 @@ void HipComm::flush() {
       const HipWorker& w = w_[size_t(rank - 1)];
       uint8_t* slot = b_.isendbuf + size_t(w.slot) * b_.sl;
       if (w.remote) {
-        xb.reserve(2, 1);
+        xb.reserve(2, 2);
         xb.copy(b_.sendbuf, slot, b_.sl);
         xb.copy(b_.sendbuf, msg_dst(w), b_.sl);
         xb.door(w.box_door_dev, w.seq);
+        if (w.path_dev) xb.door(peer_door(w), w.seq);
       } else {
         xb.copy(b_.sendbuf, slot, b_.sl);
       }
@@ -410,26 +414,32 @@ bool HipComm::fused_ok(const UpdateSpec& u, const std::vector<int64_t>& posted) 
     return false;
   size_t ndst = 0, ndoor = 0;
   for (int64_t rank : posted) {
-    const bool remote = w_[size_t(rank - 1)].remote;
-    ndst += remote ? 2 : 1;
-    ndoor += remote ? 1 : 0;
+    const HipWorker& w = w_[size_t(rank - 1)];
+    ndst += w.remote ? 2 : 1;
+    ndoor += w.remote ? (w.path_dev ? 2 : 1) : 0;
   }
   return ndst <= size_t(kMaxEpochDst) && ndoor <= size_t(kMaxDoorbells);
 }
 
 bool HipComm::tail_fits(const std::vector<int64_t>& posted, const UpdateSpec& u) const {
-  if (!fused_tail_ || posted.empty() || posted.size() > size_t(kMaxLsqTasks) || u.msg_bf16 || u.mirror) return false;
+  if (!fused_tail_ || posted.empty() || u.msg_bf16 || u.mirror) return false;
   int cp = -1;
+  size_t local = 0, remote = 0;
   for (int64_t rank : posted) {
     const HipWorker& w = w_[size_t(rank - 1)];
+    if (w.remote) {  // rank 0: the tail waits for its completion word and rings its doorbells
+      ++remote;
+      continue;
+    }
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
-    if (w.remote || ts.kind != MPA_TASK_LSQ || !ts.delays_ns.empty() || ts.dtype != u.dtype) return false;
+    if (ts.kind != MPA_TASK_LSQ || !ts.delays_ns.empty() || ts.dtype != u.dtype) return false;
     const int c = lsq_cols_pad(ts.dtype, int(ts.cols));
     if (c > kLsqWideSlice) return false;  // wide rows: two launches, no fused tail
     if (cp >= 0 && c != cp) return false;
     cp = c;
+    ++local;
   }
-  return true;
+  return local >= 1 && local <= size_t(kMaxLsqTasks) && remote <= size_t(kMaxEpochChunks);
 }
 
 void HipComm::emit_epoch(const std::vector<Harvest>& hv, size_t before, const std::vector<int64_t>& posted,
@@ -489,6 +499,10 @@ EpochArgs HipComm::epoch_args(const std::vector<Harvest>& hv, size_t before, con
       a.dst[a.ndst++] = msg_dst(w);
       a.door[a.ndoor] = w.box_door_dev;
       a.doorval[a.ndoor++] = w.seq;
+      if (w.path_dev) {  // the device doorbell a device-armed task of the worker waits on
+        a.door[a.ndoor] = peer_door(w);
+        a.doorval[a.ndoor++] = w.seq;
+      }
     }
   }
   return a;
@@ -526,7 +540,7 @@ void HipComm::maybe_ahead() {
   ww.spin_ticks = spin_ticks();
   for (const auto& cp : call_posts_) {
     HipWorker& w = w_[size_t(cp.rank - 1)];
-    if (w.remote) {
+    if (w.remote && !tail_pending_) {  // (a pending tail waited for them in the previous launch)
       if (g_wait_value_ops) {
         HIPCHECK(hipStreamWaitValue64(coord_, region_->dev(&w.box->done), w.seq, hipStreamWaitValueGte, ~0ull));
       } else {
@@ -550,7 +564,20 @@ void HipComm::maybe_ahead() {
   // step in its last workgroup and the next maybe_ahead enqueues only the launch
   if (more && tail_fits(posted, u)) {
     tail_args_ = epoch_args(hv, hv.size(), posted, u);
-    tail_ranks_ = posted.size();
+    // the tail dispatches the epoch after this one: remote doorbells take its task numbers,
+    // and it first waits for this epoch's remote completions
+    for (int d = 0; d < tail_args_.ndoor; ++d) tail_args_.doorval[d] += 1;
+    tail_ranks_ = 0;
+    tail_nwait_ = 0;
+    for (int64_t rank : posted) {
+      const HipWorker& w = w_[size_t(rank - 1)];
+      if (!w.remote) {
+        ++tail_ranks_;
+        continue;
+      }
+      tail_word_[tail_nwait_] = region_->dev(&w.box->done);
+      tail_target_[tail_nwait_++] = w.seq;
+    }
     tail_next_ = true;
     tail_pending_ = true;
   }

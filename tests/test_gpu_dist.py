@@ -56,7 +56,7 @@ def test_lsq_two_processes_prearmed(built, monkeypatch):
 
 @pytest.mark.parametrize("arm", ["0", "2"])
 def test_lsqb_two_processes(built, monkeypatch, arm):
-    """The batched variant across processes, host-launched (default) and pre-armed."""
+    """The batched variant across processes, host-launched and device-armed (default)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -65,13 +65,14 @@ def test_lsqb_two_processes(built, monkeypatch, arm):
 
 
 @pytest.mark.parametrize("placement,env", [
-    ([0, 1, 1, 1], {}),                                   # rank 1 serves 3 workers (host-launched)
-    ([0, 1], {}),                                         # one worker per process, host-launched
-    ([0, 1], {"MPA_ARM": "2"}),                           # ... pre-armed (opt-in)
+    ([0, 1, 1, 1], {}),                                   # rank 1 serves 3 workers (host-launched, one batch)
+    ([0, 1, 1, 1], {"MPA_ARM": "1"}),                     # ... each device-armed
+    ([0, 1], {}),                                         # one worker per process: device-armed (default)
+    ([0, 1], {"MPA_ARM": "0"}),                           # ... host-launched
     ([0, 1, 1], {"MPA_AHEAD": "0"}),                      # fused epoch kernel, no launch-ahead
     ([0, 1], {"MPA_FUSE": "0"}),                          # the unfused loop
     ([0, 1, 1], {"MPA_XGMI": "0"}),                       # payloads through the host mailbox
-    ([0, 1], {"MPA_XGMI": "0", "MPA_ARM": "2"}),          # ... pre-armed
+    ([0, 1], {"MPA_XGMI": "0", "MPA_ARM": "2"}),          # ... never armed (host mailbox)
 ])  # (MPA_WAIT_VALUE_OPS / MPA_GATHER, A/B switches, exist in the measurement build only)
 def test_lsq_descent_two_processes(built, placement, env):
     import torch
