@@ -149,6 +149,15 @@ struct LsqBatch {
   EpochArgs ep;
 };
 static_assert(sizeof(LsqBatch) <= 4096, "LsqBatch is passed by value as kernel arguments (4 KiB)");
+// A batch with a device-armed task launches the kernel variant whose workgroups wait on the
+// doorbell first; every other launch runs a variant without that prologue (its mere presence
+// cost the c2 launch 19 %: profiles/r03_cross_tail.txt)
+template <class Batch>
+inline bool batch_armed(const Batch& b) {
+  for (int k = 0; k < b.ntasks; ++k)
+    if (b.t[k].door) return true;
+  return false;
+}
 // Returns hipErrorInvalidValue if no kernel variant covers (dtype, cols).  cols > 2048 runs
 // the wide two passes (launch_lsqw).
 hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s);

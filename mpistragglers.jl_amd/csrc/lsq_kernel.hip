@@ -30,6 +30,8 @@
 //   M_BLOCKED   each workgroup streams ONE contiguous row range (its 1/grid of the task,
 //               in whole tiles), its waves taking the range's tiles in turn, instead of
 //               the grid sweeping the task's rows together
+//   M_ARMED     (set per launch, not a tuning bit) every workgroup first waits on the task's
+//               device doorbell (a device-armed task of a worker process, kernels.hpp)
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -49,7 +51,7 @@ namespace {
 
 using namespace dev;
 
-enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16, M_BLOCKED = 32 };
+enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16, M_BLOCKED = 32, M_ARMED = 64 };
 
 template <typename T, int VPL, int RB, int MODE>
 struct Tile {
@@ -123,7 +125,8 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   while (ti + 1 < batch.ntasks && int(blockIdx.x) >= batch.block0[ti + 1]) ++ti;
   const LsqTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block0[ti];
-  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed
+  if constexpr ((MODE & M_ARMED) != 0)
+    if (!wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed
   // A pre-armed task its server cancelled (the host-memory go word holds its seq) computes
   // but neither writes its reply nor publishes.  The word is read ONCE, by the workgroup that
   // writes the reply, at that point: every lane of every workgroup reading it before any work
@@ -362,7 +365,8 @@ template <typename T, int VPL, int RB, int MODE>
 hipError_t go(const LsqBatch& a, hipStream_t s) {
   const int grid = a.block0[a.ntasks];
   if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL((lsq_grad_kernel<T, VPL, RB, MODE>), dim3(grid), dim3(kThreads), 0, s, a);
+  if (batch_armed(a)) hipLaunchKernelGGL((lsq_grad_kernel<T, VPL, RB, MODE | M_ARMED>), dim3(grid), dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL((lsq_grad_kernel<T, VPL, RB, MODE>), dim3(grid), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -88,12 +88,14 @@ constexpr int P1_KC = 128;          // X rows per LDS chunk = 4 k-steps of 32
 constexpr int P1_XS = K * 2 + 16;   // LDS bytes per X row (pad: 2-way tr reads at most)
 constexpr int P1_WG_ROWS = 256;     // 8 waves x 32 rows
 
+template <bool ARMED>
 __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_chunked_kernel(LsqbBatch batch) {
   __shared__ __attribute__((aligned(16))) uint8_t xs[2][P1_KC * P1_XS];
   const int ti = task_of(batch.block1, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block1[ti];
-  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed (pass 2 follows on the stream)
+  if constexpr (ARMED)  // device-armed (pass 2 follows on the stream)
+    if (!wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;
   if (disarmed(a.go, a.seq)) return;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -245,13 +247,15 @@ constexpr int Q_STAGE = 32 * Q_XS;         // one wave's staging window (one k-s
 constexpr int Q_PK = K + 4;                // partial-residual row stride (floats; conflict-free)
 constexpr int Q_PART = Q_ROWS * Q_PK * 4;  // one wave's partial residual (fp32)
 
+template <bool ARMED>
 __global__ void __launch_bounds__(P1_THREADS) lsqb_resid_kernel(LsqbBatch batch) {
   constexpr int LDS = (8 * Q_STAGE > 8 * Q_PART ? 8 * Q_STAGE : 8 * Q_PART);
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
   const int ti = task_of(batch.block1, batch.ntasks);
   const LsqbTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block1[ti];
-  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed (pass 2 follows on the stream)
+  if constexpr (ARMED)  // device-armed (pass 2 follows on the stream)
+    if (!wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;
   if (disarmed(a.go, a.seq)) return;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -553,8 +557,11 @@ __global__ void __launch_bounds__(kThreads, 2) lsqb_grad_kernel(LsqbBatch batch)
 hipError_t launch_lsqb(const LsqbBatch& a, hipStream_t s) {
   const int g1 = a.block1[a.ntasks], g2 = a.block2[a.ntasks];
   if (g1 <= 0 || g2 <= 0) return hipErrorInvalidValue;
-  if (a.splitk) hipLaunchKernelGGL(lsqb_resid_kernel, dim3(g1), dim3(P1_THREADS), 0, s, a);
-  else hipLaunchKernelGGL(lsqb_resid_chunked_kernel, dim3(g1), dim3(P1_THREADS), 0, s, a);
+  const bool armed = batch_armed(a);
+  if (a.splitk && armed) hipLaunchKernelGGL(lsqb_resid_kernel<true>, dim3(g1), dim3(P1_THREADS), 0, s, a);
+  else if (a.splitk) hipLaunchKernelGGL(lsqb_resid_kernel<false>, dim3(g1), dim3(P1_THREADS), 0, s, a);
+  else if (armed) hipLaunchKernelGGL(lsqb_resid_chunked_kernel<true>, dim3(g1), dim3(P1_THREADS), 0, s, a);
+  else hipLaunchKernelGGL(lsqb_resid_chunked_kernel<false>, dim3(g1), dim3(P1_THREADS), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(lsqb_grad_kernel, dim3(g2), dim3(kThreads), 0, s, a);

@@ -134,6 +134,7 @@ __device__ __forceinline__ f32x4 ld_wt(const f32x4* p) {
   return __builtin_bit_cast(f32x4, u);
 }
 
+template <bool ARMED>
 __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[QW][2][SLICE];
   __shared__ __attribute__((aligned(16))) uint8_t bring[2][PRB * PH * 2];
@@ -156,7 +157,8 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   // every workgroup before any work (profiles/r02_arm_go_word.txt)
   const int q = pidx - batch.grp0[ti];
   const int ng = batch.grp0[ti + 1] - batch.grp0[ti];
-  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed
+  if constexpr (ARMED)
+    if (!wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed
 
   const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
   const int qq = (lane >> 2) & 3, p4 = lane & 3;
@@ -534,7 +536,8 @@ hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s) {
   const int pairs = a.grp0[a.ntasks];
   if (pairs <= 0) return hipErrorInvalidValue;
   const int grid = (pairs + 7) / 8 * 16;
-  hipLaunchKernelGGL(lsqp4_kernel, dim3(grid), dim3(QT), 0, s, a);
+  if (batch_armed(a)) hipLaunchKernelGGL(lsqp4_kernel<true>, dim3(grid), dim3(QT), 0, s, a);
+  else hipLaunchKernelGGL(lsqp4_kernel<false>, dim3(grid), dim3(QT), 0, s, a);
   return hipGetLastError();
 }
 

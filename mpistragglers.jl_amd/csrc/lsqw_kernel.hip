@@ -41,7 +41,7 @@ __device__ __forceinline__ Pack<T> x_vec(const T* __restrict__ x, int v, int col
   return p;
 }
 
-template <typename T>
+template <typename T, bool ARMED>
 __global__ void __launch_bounds__(kThreads) lsqw_resid_kernel(LsqBatch batch) {
   using P = Pack<T>;
   constexpr int E = P::E;
@@ -49,7 +49,8 @@ __global__ void __launch_bounds__(kThreads) lsqw_resid_kernel(LsqBatch batch) {
   while (ti + 1 < batch.ntasks && int(blockIdx.x) >= batch.block0[ti + 1]) ++ti;
   const LsqTask& a = batch.t[ti];
   const int blk = int(blockIdx.x) - batch.block0[ti];
-  if (a.door && !wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed (pass 2 follows on the stream)
+  if constexpr (ARMED)  // device-armed (pass 2 follows on the stream)
+    if (!wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;
   if (disarmed(a.go, a.seq)) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
@@ -239,10 +240,12 @@ hipError_t launch_lsqw(int dtype, const LsqBatch& a, hipStream_t s) {
   }
   if (grid1 <= 0) return hipErrorInvalidValue;
   if (dtype == MPA_F32) {
-    hipLaunchKernelGGL(lsqw_resid_kernel<float>, dim3(grid1), dim3(kThreads), 0, s, a);
+    if (batch_armed(a)) hipLaunchKernelGGL((lsqw_resid_kernel<float, true>), dim3(grid1), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((lsqw_resid_kernel<float, false>), dim3(grid1), dim3(kThreads), 0, s, a);
     hipLaunchKernelGGL((lsqw_grad_kernel<float, 8, 2>), dim3(grid2), dim3(kThreads), 0, s, a);
   } else if (dtype == MPA_F64) {
-    hipLaunchKernelGGL(lsqw_resid_kernel<double>, dim3(grid1), dim3(kThreads), 0, s, a);
+    if (batch_armed(a)) hipLaunchKernelGGL((lsqw_resid_kernel<double, true>), dim3(grid1), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((lsqw_resid_kernel<double, false>), dim3(grid1), dim3(kThreads), 0, s, a);
     hipLaunchKernelGGL((lsqw_grad_kernel<double, 16, 1>), dim3(grid2), dim3(kThreads), 0, s, a);
   } else {
     return hipErrorInvalidValue;

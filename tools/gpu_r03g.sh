@@ -27,3 +27,5 @@ for cfg in c1 c2; do
 done
 timeout -k 10 300 python -u bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baseline > $O/c5.log 2>&1 || exit $?
 grep '^{' $O/c5.log > $O/c5.json; echo "c5 $(python3 -c "import json;d=json.load(open('$O/c5.json'));r=d['roofline'];print(d['value'], d['ms_per_step'], r['avg_launch_ms'], r['frac'])")"
+timeout -k 10 120 tools/bin/probe_dma_issue > $O/probe.txt 2>&1 || exit $?
+tail -8 $O/probe.txt

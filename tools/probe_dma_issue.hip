@@ -27,7 +27,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
     if (e_) { std::printf("FAIL %s: %s\n", #x, hipGetErrorString(e_)); std::exit(1); } \
   } while (0)
 
-template <int FORM, int D, bool MF = true>
+template <int FORM, int D, bool MF = true, int VM = 24>
 __global__ void __launch_bounds__(256, 1) probe(const uint8_t* __restrict__ buf, size_t bytes, int steps, float* out) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[4][16384];
   const int lane = threadIdx.x & 63;
@@ -69,8 +69,14 @@ __global__ void __launch_bounds__(256, 1) probe(const uint8_t* __restrict__ buf,
           off += 1024;
           if (off + 1024 > per_wave) off = 0;
           ++piece;
-          // bound the loads in flight (the kernel keeps ~20-34): wait for all but 24
-          if ((piece & 7) == 0) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+          // bound the loads in flight (the kernel keeps ~20-34): wait for all but VM
+          if ((piece & 7) == 0) {
+            if (VM == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (VM == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else if (VM == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+            else if (VM == 54) asm volatile("s_waitcnt vmcnt(54)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+          }
         }
       }
     }
@@ -84,17 +90,17 @@ __global__ void __launch_bounds__(256, 1) probe(const uint8_t* __restrict__ buf,
   if (s == 1234.5f) out[threadIdx.x] = s;  // never true; keeps the work alive
 }
 
-template <int FORM, int D, bool MF = true>
+template <int FORM, int D, bool MF = true, int VM = 24>
 double run(const uint8_t* buf, size_t bytes, int steps, float* out, int grid) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  probe<FORM, D, MF><<<grid, 256>>>(buf, bytes, 4, out);  // warm-up
+  probe<FORM, D, MF, VM><<<grid, 256>>>(buf, bytes, 4, out);  // warm-up
   CK(hipDeviceSynchronize());
   double best = 1e30;
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipEventRecord(a));
-    probe<FORM, D, MF><<<grid, 256>>>(buf, bytes, steps, out);
+    probe<FORM, D, MF, VM><<<grid, 256>>>(buf, bytes, steps, out);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms = 0;
@@ -125,8 +131,7 @@ int main() {
       {"glds vaddr64 D=4 ", run<2, 4>, 4, true},   {"buf offen    D=4 ", run<3, 4>, 4, true},
       {"glds no-MFMA D=16", run<1, 16, false>, 16, false},
   };
-  const struct { const char* where; size_t bytes; } places[] = {
-      {"HBM 4 GiB", big}, {"MALL 128 MiB", size_t(128) << 20}, {"L2 16 MiB", size_t(16) << 20}};
+  const struct { const char* where; size_t bytes; } places[] = {{"HBM 4 GiB", big}};
   for (const auto& pl : places) {
     std::printf("-- buffer %s (%.0f KiB per wave)\n", pl.where, double(pl.bytes) / (grid * 4) / 1024);
     for (const R& r : rs) {
@@ -136,6 +141,19 @@ int main() {
       std::printf("%s %.3f ms  %.1f ns/step  +%.1f ns per DMA over MFMA-only  %.0f GB/s chip = %.1f GB/s per CU\n",
                   r.name, t, per_step_ns, extra_ns, gbs, gbs / grid);
     }
+  }
+  // loads in flight: the wave waits for all but VM of its DMAs every 8 (HBM buffer)
+  const R vs[] = {{"glds saddr   D=8  vm8 ", run<1, 8, true, 8>, 8, true},
+                  {"glds saddr   D=8  vm16", run<1, 8, true, 16>, 8, true},
+                  {"glds saddr   D=8  vm24", run<1, 8, true, 24>, 8, true},
+                  {"glds saddr   D=8  vm40", run<1, 8, true, 40>, 8, true},
+                  {"glds saddr   D=8  vm54", run<1, 8, true, 54>, 8, true},
+                  {"glds no-MFMA D=16 vm54", run<1, 16, false, 54>, 16, false}};
+  std::printf("-- loads in flight, buffer HBM 4 GiB\n");
+  for (const R& r : vs) {
+    const double t = r.f(buf, big, steps, out, grid);
+    const double gbs = double(steps) * r.d * 1024.0 * grid * 4 / (t * 1e-3) / 1e9;
+    std::printf("%s %.3f ms  %.0f GB/s chip = %.1f GB/s per CU\n", r.name, t, gbs, gbs / grid);
   }
   std::printf("ok\n");
   return 0;
