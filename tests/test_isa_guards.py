@@ -1,0 +1,57 @@
+"""ISA guards of the product kernels that write M0 themselves (CPU: hipcc cross-compiles gfx950).
+
+lsqp4_kernel.hip issues its LDS-DMAs (`global_load_lds_dword[x4]`) from inline asm that loads
+the LDS destination into M0.  Two rules keep that correct without saving M0 around every DMA
+(saving it cost c5 1.5-2.5 %, profiles/r03_dma_asm_ab.txt):
+  * the SALU write of M0 and the DMA reading it are one wait state apart (`s_nop 0`);
+  * the compiler itself never touches M0 in these kernels, so nothing it emits can see the
+    value the asm leaves there (checked here on the generated code, so a compiler or source
+    change that starts using M0 fails this test instead of corrupting LDS silently).
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "mpistragglers.jl_amd", "csrc")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+def _asm(tmp_path, src):
+    out = tmp_path / (os.path.basename(src) + ".s")
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "--offload-device-only", "-S",
+           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, os.path.join(CSRC, src), "-o", str(out)]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    return out.read_text()
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_lsqp4_m0_writes_are_separated_and_private(tmp_path):
+    text = _asm(tmp_path, "lsqp4_kernel.hip")
+    in_asm = False
+    prev = None
+    m0_writes = dma = 0
+    for raw in text.splitlines():
+        line = raw.split(";")[0].strip()
+        if raw.strip().startswith(";;#ASMSTART"):
+            in_asm, prev = True, None
+            continue
+        if raw.strip().startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if not line or line.startswith("."):
+            continue
+        mentions_m0 = re.search(r"\bm0\b", line) is not None
+        if not in_asm:
+            assert not mentions_m0, f"compiler-emitted instruction uses M0: {line}"
+            continue
+        if line.startswith("s_mov_b32 m0,"):
+            m0_writes += 1
+        if line.startswith("global_load_lds"):
+            dma += 1
+            assert prev == "s_nop 0", f"LDS-DMA right after the M0 write without a wait state: {prev!r} -> {line}"
+        prev = line
+    assert m0_writes > 0 and dma == m0_writes
