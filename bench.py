@@ -302,8 +302,13 @@ def report(args, cfg, world, el, per_rank, extra):
         "epoch_alg_GBps": round(epoch_bytes * its / 1e9, 1),
     }
     if rocprof:
-        out["roofline"]["rocprof_avg_launch_ms"], out["roofline"]["rocprof_source"] = rocprof
-        out["roofline"]["rocprof_frac"] = round(per_launch_bytes / (rocprof[0] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+        # figures of an EARLIER traced run of this command, kept apart from this run's
+        # measurements and labelled with the tree they were taken on (they go stale
+        # silently when the kernel changes)
+        avg_ms, src, tree = rocprof
+        out["roofline"]["committed_profiles"] = {
+            "rocprof_avg_launch_ms": avg_ms, "source": src, "tree_commit": tree,
+            "rocprof_frac": round(per_launch_bytes / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
     rp = extra.pop("measured_read_peak", None)
     if rp:
         out["roofline"]["measured_read_peak"] = rp
@@ -312,21 +317,23 @@ def report(args, cfg, world, el, per_rank, extra):
     return out
 
 
-ROCPROF_STATS = {"c2": ("r02_c2_kernel_stats.csv", "lsq_grad_kernel"),
-                 "c5": ("r02_c5_kernel_stats.csv", "lsqp4_kernel")}
+ROCPROF_STATS = {"c2": ("r03_c2_kernel_stats.csv", "lsq_grad_kernel"),
+                 "c5": ("r03_c5_kernel_stats.csv", "lsqp4_kernel")}
 
 
 def rocprof_avg_ms(cfg):
-    """(average ms, source) of the dominant kernel under rocprofv3 in the committed profiles
-    of this config's bench command: the timed-region window of its kernel trace
-    (tools/trace_window.py) where committed, else the --stats summary; None without either."""
+    """(average ms, source, tree commit) of the dominant kernel under rocprofv3 in the committed
+    profiles of this config's bench command: the timed-region window of its kernel trace
+    (tools/trace_window.py) of the newest round that has one, else the --stats summary; None
+    without either."""
     name, kernel = ROCPROF_STATS.get(cfg["config"], (None, None))
-    win = os.path.join(ROOT, "profiles", "r02_%s_rocprof_window.json" % cfg["config"])
-    if name and os.path.exists(win):
-        d = json.load(open(win))
-        if d.get("kernel") == kernel:
-            return round(d["avg_ms"], 4), "profiles/%s (last %d launches of the traced run = its timed region; %s)" % (
-                os.path.basename(win), d["launches"], d.get("date", ""))
+    for rnd in ("r03", "r02"):
+        win = os.path.join(ROOT, "profiles", "%s_%s_rocprof_window.json" % (rnd, cfg["config"]))
+        if name and os.path.exists(win):
+            d = json.load(open(win))
+            if d.get("kernel") == kernel:
+                return round(d["avg_ms"], 4), "profiles/%s (last %d launches of the traced run = its timed region; %s)" % (
+                    os.path.basename(win), d["launches"], d.get("date", "")), d.get("tree_commit")
     path = os.path.join(ROOT, "profiles", name) if name else None
     if not path or not os.path.exists(path):
         return None
@@ -334,7 +341,7 @@ def rocprof_avg_ms(cfg):
     with open(path) as f:
         for row in csv.DictReader(f):
             if kernel in row["Name"]:
-                return round(float(row["AverageNs"]) / 1e6, 4), "profiles/%s (%s calls)" % (name, row["Calls"])
+                return round(float(row["AverageNs"]) / 1e6, 4), "profiles/%s (%s calls)" % (name, row["Calls"]), None
     return None
 
 

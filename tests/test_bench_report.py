@@ -72,10 +72,14 @@ def test_provenance_fields():
     assert "HIP events" in r["avg_launch_ms_source"]
     if r["traffic"] is not None:
         assert r["traffic_source"].startswith("profiles/lsq_pmc_c2.json") and "not this run" in r["traffic_source"]
-    if "rocprof_avg_launch_ms" in r:
-        ms = r["rocprof_avg_launch_ms"]
-        assert r["rocprof_source"].startswith("profiles/")
-        assert abs(r["rocprof_frac"] - alg / (ms / 1e3) / 1e9 / 8000.0) < 1e-3
+    # figures of an earlier traced run sit in their own sub-object, never beside
+    # this run's measurements, with the tree they were taken on
+    assert "rocprof_avg_launch_ms" not in r and "rocprof_frac" not in r
+    cp = r.get("committed_profiles")
+    assert cp is not None  # profiles/r03_c2_rocprof_window.json is committed
+    ms = cp["rocprof_avg_launch_ms"]
+    assert cp["source"].startswith("profiles/") and cp["tree_commit"]
+    assert abs(cp["rocprof_frac"] - alg / (ms / 1e3) / 1e9 / 8000.0) < 1e-3
 
 
 def test_cpu_baseline_records_host(monkeypatch, tmp_path):
