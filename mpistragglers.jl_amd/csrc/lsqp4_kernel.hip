@@ -105,6 +105,23 @@ __device__ __forceinline__ void dma16(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(l) : "memory");
 }
+// the saddr forms with an immediate offset (FULL blocks): the instruction adds OFF to the
+// global address AND to the LDS address (llvm.amdgcn.global.load.lds: "applied to both"), so
+// m0 = LDS destination - OFF.  One scalar base per block instead of a 64-bit add per strip
+template <int OFF>
+__device__ __forceinline__ void dma_off(const void* sbase, uint32_t voff, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds))) - uint32_t(OFF);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 offset:%3" ::"v"(voff), "s"(sbase), "s"(l),
+               "i"(OFF) : "memory");
+}
+__device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l) : "memory");
+}
+__device__ __forceinline__ void pf4_s(const void* sbase, uint32_t voff, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(l) : "memory");
+}
 
 // 16-B chunk c of strip row r sits at chunk position c ^ sw(r) (bits 1-2 only: chunk pairs
 // stay together); found by search over the linear maps of r's bits for conflict-free reads of
@@ -128,7 +145,10 @@ __device__ __forceinline__ f32x4 ld_wt(const f32x4* p) {
   return __builtin_bit_cast(f32x4, u);
 }
 
-template <bool ARMED>
+// FULL: every task of the batch has cols == 2048 and rows % 16 == 0 (BASELINE c5's shape):
+// no ragged block, no partial strip, so the block loop drops the clamps, selects and masks
+// of the general form and addresses a block from ONE scalar base (immediate strip offsets)
+template <bool ARMED, bool FULL>
 __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[QW][2][SLICE];
   __shared__ __attribute__((aligned(16))) uint8_t bring[2][PRB * PH * 2];
@@ -240,11 +260,31 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   // 0 .. 31 (finite data that meets X = 0; their G columns are never stored)
   auto dma_strip = [&](const Blk& b, const uint32_t (&vf)[2], const uint32_t (&vp)[2], int k, uint8_t* slot)
       __attribute__((always_inline)) {
-    const int cb = c0 + 64 * k;
-    const bool full = cb + 64 <= cols;
-    const uint16_t* base = b.p + (cb < cols ? cb : 0);
+    if constexpr (FULL) {
+      // every strip of every block lies inside the rows: base = the block's first row at c0,
+      // strip k at the immediate offset 128 k (k is a constant once the loops are unrolled)
+      const uint16_t* base = b.p + c0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dma_row(base, full ? vf[j] : vp[j], slot + 2048 * k + 1024 * j);
+      for (int j = 0; j < 2; ++j) {
+        uint8_t* d = slot + 2048 * k + 1024 * j;
+        switch (k) {
+          case 0: dma_off<0>(base, vf[j], d); break;
+          case 1: dma_off<128>(base, vf[j], d); break;
+          case 2: dma_off<256>(base, vf[j], d); break;
+          case 3: dma_off<384>(base, vf[j], d); break;
+          case 4: dma_off<512>(base, vf[j], d); break;
+          case 5: dma_off<640>(base, vf[j], d); break;
+          case 6: dma_off<768>(base, vf[j], d); break;
+          default: dma_off<896>(base, vf[j], d); break;
+        }
+      }
+    } else {
+      const int cb = c0 + 64 * k;
+      const bool full = cb + 64 <= cols;
+      const uint16_t* base = b.p + (cb < cols ? cb : 0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma_row(base, full ? vf[j] : vp[j], slot + 2048 * k + 1024 * j);
+    }
   };
   auto dma = [&](int64_t kb, uint8_t* slot) __attribute__((always_inline)) {
     const Blk b = blk(kb);
@@ -259,22 +299,34 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   // re-touches the block being loaded), so every wait counts the same loads
   const int pfd = batch.pfd;
   const uint32_t pfoff = uint32_t(c0 + 64 * (lane & 7) < cols ? c0 + 64 * (lane & 7) : 0) * 2u;
+  const uint32_t pfv = uint32_t(lane >> 3) * uint32_t(lda) * 2u + pfoff;  // FULL: lane offset from row 8h
   auto pf = [&](int64_t kb) __attribute__((always_inline)) {
     const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
-    int64_t row = kc * PRB + 8 * h + (lane >> 3);
-    row = row < rows ? row : rows - 1;
-    pf4(reinterpret_cast<const uint8_t*>(A + row * lda) + pfoff, &sink[w][0]);
+    if constexpr (FULL) {
+      pf4_s(A + (kc * PRB + 8 * h) * lda, pfv, &sink[w][0]);
+    } else {
+      int64_t row = kc * PRB + 8 * h + (lane >> 3);
+      row = row < rows ? row : rows - 1;
+      pf4(reinterpret_cast<const uint8_t*>(A + row * lda) + pfoff, &sink[w][0]);
+    }
   };
   // B of a block (16 rows x 32 iterates of half h = 16 x 64 B): one instruction of wave 0; the
   // other waves touch the same rows into their sink instead, so every wave counts one load
   const int brow = lane >> 2, bpiece = lane & 3;
+  const uint32_t bv = uint32_t(brow * K + 8 * bpiece) * 2u;  // FULL: lane offset from the block's first B row
   auto dma_b = [&](int64_t kb, uint8_t* bslot) __attribute__((always_inline)) {
     const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
-    int64_t row = kc * PRB + brow;
-    row = row < rows ? row : rows - 1;
-    const uint16_t* src = Bm + row * K + PH * h + 8 * bpiece;
-    if (w == 0) dma16(src, bslot);
-    else pf4(src, &sink[w][0]);
+    if constexpr (FULL) {
+      const uint16_t* sb = Bm + kc * PRB * K + PH * h;
+      if (w == 0) dma16_s(sb, bv, bslot);
+      else pf4_s(sb, bv, &sink[w][0]);
+    } else {
+      int64_t row = kc * PRB + brow;
+      row = row < rows ? row : rows - 1;
+      const uint16_t* src = Bm + row * K + PH * h + 8 * bpiece;
+      if (w == 0) dma16(src, bslot);
+      else pf4(src, &sink[w][0]);
+    }
   };
   // vmcnt(n) alone (expcnt / lgkmcnt fields left free)
 #define MPA_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
@@ -323,18 +375,26 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     for (int c4 = 0; c4 < 4; ++c4) off2[c4] = r0 * 128 + ((2 * c4 + (p4 >> 1)) ^ sw(r0)) * 16 + 8 * (p4 & 1);
   }
 
+  // -I as the B operand of iterate tile t: lane (i, g) holds k = 8g .. 8g + 7 of column n = i
+  bf16x8 NEGI[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) NEGI[t][j] = (8 * g + j == 16 * t + i) ? (__bf16)(-1.0f) : (__bf16)(0.0f);
+
   auto step = [&](int u, uint8_t* slot, uint8_t* bslot, f32x4 (&pt)[QW][2][64]) __attribute__((always_inline)) {
     // ---- phase 1: P_w[rows 4g + r][iterate 16 t + i].  Fragment reads run AD k-steps ahead
     // of the MFMAs, each strip's after its wait
     constexpr int AD = MPA_LSQP4_AD;
     wait_strip((AD - 1) / 2);  // the strips of the first AD k-steps (and B, older)
     f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    if (w == 0) {  // wave 0 DMA'd B: its accumulators start at -B
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          p1[t][r] = -bf16_f32(*reinterpret_cast<const uint16_t*>(bslot + (4 * g + r) * (PH * 2) + 2 * (16 * t + i)));
+    if (w == 0) {
+      // wave 0 DMA'd B: its accumulators start at -B, by one MFMA per iterate tile of the B rows
+      // (A operand: lane (i, g) = row i, iterates 8g .. 8g + 7 of the half, one 16-B read of the
+      // row-major slot) against -I (exact: one nonzero product per output, added to 0)
+      const bf16x8 bfr = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(bslot + i * (PH * 2) + 16 * g));
+      p1[0] = mfma(bfr, NEGI[0], p1[0]);
+      p1[1] = mfma(bfr, NEGI[1], p1[1]);
     }
     {
     bf16x8 af[AD];
@@ -381,7 +441,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     barrier();
     {
       const int64_t row0 = (kb0 + u) * PRB + 4 * g;
-      const bool ragged = (kb0 + u + 1) * PRB > rows;  // wave-uniform
+      const bool ragged = !FULL && (kb0 + u + 1) * PRB > rows;  // wave-uniform
       f32x4 pv[2][QW];  // all eight reads in flight at once
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -530,8 +590,13 @@ hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s) {
   const int pairs = a.grp0[a.ntasks];
   if (pairs <= 0) return hipErrorInvalidValue;
   const int grid = (pairs + 7) / 8 * 16;
-  if (batch_armed(a)) hipLaunchKernelGGL(lsqp4_kernel<true>, dim3(grid), dim3(QT), 0, s, a);
-  else hipLaunchKernelGGL(lsqp4_kernel<false>, dim3(grid), dim3(QT), 0, s, a);
+  bool full = true;
+  for (int t = 0; t < a.ntasks; ++t) full = full && a.t[t].cols == kLsqpMaxCols && a.t[t].rows % PRB == 0;
+  const bool armed = batch_armed(a);
+  if (armed && full) hipLaunchKernelGGL((lsqp4_kernel<true, true>), dim3(grid), dim3(QT), 0, s, a);
+  else if (armed) hipLaunchKernelGGL((lsqp4_kernel<true, false>), dim3(grid), dim3(QT), 0, s, a);
+  else if (full) hipLaunchKernelGGL((lsqp4_kernel<false, true>), dim3(grid), dim3(QT), 0, s, a);
+  else hipLaunchKernelGGL((lsqp4_kernel<false, false>), dim3(grid), dim3(QT), 0, s, a);
   return hipGetLastError();
 }
 

@@ -230,3 +230,30 @@ def test_single_pass_vs_oracle(M, monkeypatch, env, rows, cols, n):
     again, _, _, _ = _run(M, torch, shards, cols, X, comm=comm, pool=pool, bufs=comm._bufs)
     assert np.array_equal(again.view(np.uint32), out.view(np.uint32))
     comm.close()
+
+
+def test_lsqp4_full_form_matches_general_form_bitwise(M):
+    """lsqp4_kernel's FULL form (every task of the batch has cols = 2048 and rows % 16 = 0:
+    immediate-offset strip DMAs, no clamps or masks, -B folded into one MFMA per tile) against
+    the oracle and bit for bit against the general form: the same two 4800-row shards run once
+    in a batch of their own (FULL) and once beside a third, ragged shard (general form); the
+    row groups per task are equal in both batches, so the G trees sum in the same order."""
+    import lsq
+    import torch
+    rows, cols = 4800, 2048
+    A, B, X = _problem(3 * rows, cols, seed=77)
+    full = [(A[i * rows:(i + 1) * rows], B[i * rows:(i + 1) * rows]) for i in range(2)]
+    # a third shard makes the batch general: 4799 rows (ragged); 3 tasks in both batches
+    shards_f = full + [(A[2 * rows:3 * rows], B[2 * rows:3 * rows])]
+    shards_g = full + [(A[2 * rows:3 * rows - 1], B[2 * rows:3 * rows - 1])]
+    out_f, rep, comm, _ = _run(M, torch, shards_f, cols, X)
+    comm.close()
+    out_g, rep, comm, _ = _run(M, torch, shards_g, cols, X)
+    comm.close()
+    for i in range(2):
+        err = lsq.rel_err(out_f[i], lsq.batched_shard_gradient(full[i][0], full[i][1], X, "bf16"))
+        print(f"lsqp4 FULL worker {i + 1} rel err {err:.3e}")
+        assert err <= TOL, (i, err)
+        assert np.array_equal(out_f[i].view(np.uint32), out_g[i].view(np.uint32)), i
+    err = lsq.rel_err(out_g[2], lsq.batched_shard_gradient(shards_g[2][0], shards_g[2][1], X, "bf16"))
+    assert err <= TOL, err
