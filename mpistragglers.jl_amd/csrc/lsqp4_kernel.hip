@@ -52,6 +52,7 @@ namespace {
 using namespace dev;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -81,10 +82,13 @@ static_assert(NKS == 16 && NCT == 32, "8 strips of 64 columns per wave");
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-// round to nearest even by the hardware's conversion (v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint16_t bf16_cvt(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
-__device__ __forceinline__ float bf16_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xc07f); }  // lgkmcnt(0)
+// lgkmcnt(N) alone (vmcnt / expcnt fields left free)
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  static_assert(N >= 0 && N < 16, "lgkmcnt is 4 bits");
+  __builtin_amdgcn_s_waitcnt(0xc07f | (N << 8));
+}
 // workgroup barrier that leaves the vector-memory queue alone (the next block's DMA stays in
 // flight): LDS traffic drained, then s_barrier; the clobber pins LDS accesses on either side
 __device__ __forceinline__ void barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -108,11 +112,15 @@ __device__ __forceinline__ void dma16(const void* src, void* lds) {
 // the saddr forms with an immediate offset (FULL blocks): the instruction adds OFF to the
 // global address AND to the LDS address (llvm.amdgcn.global.load.lds: "applied to both"), so
 // m0 = LDS destination - OFF.  One scalar base per block instead of a 64-bit add per strip
+// A whole strip (both halves) under one M0 write: half j lands at lds + 1024 j and reads its
+// rows at voff_j, so with m0 = lds - OFF and offsets OFF and OFF + 1024 the second half's lane
+// offset is passed as voff_1 - 1024 (voff_1 >= 8 rows >= 1024 B)
 template <int OFF>
-__device__ __forceinline__ void dma_off(const void* sbase, uint32_t voff, void* lds) {
+__device__ __forceinline__ void dma_strip_off(const void* sbase, uint32_t voff0, uint32_t voff1m, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds))) - uint32_t(OFF);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 offset:%3" ::"v"(voff), "s"(sbase), "s"(l),
-               "i"(OFF) : "memory");
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2 offset:%4\n\t"
+               "global_load_lds_dwordx4 %1, %2 offset:%5"
+               ::"v"(voff0), "v"(voff1m), "s"(sbase), "s"(l), "i"(OFF), "i"(OFF + 1024) : "memory");
 }
 __device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
@@ -184,7 +192,11 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   // X = 0, their G columns are never stored): branch-free block loop
   const int nks = cols > c0 ? ((cols - c0) < QKW ? (cols - c0) : QKW) / 32 : 0;
   const int64_t nblocks = (rows + PRB - 1) / PRB;
-  const int64_t kb0 = nblocks * q / ng, kb1 = nblocks * (q + 1) / ng;
+  // wave-uniform by construction; readfirstlane keeps the block arithmetic on the scalar unit
+  // block indices in 32 bits (SALU has no 64-bit compare): the clamps below stay scalar
+  const int kb0 = __builtin_amdgcn_readfirstlane(int(nblocks * q / ng)),
+            kb1 = __builtin_amdgcn_readfirstlane(int(nblocks * (q + 1) / ng));
+  const int kblast = kb1 > kb0 ? kb1 - 1 : kb0;  // past the range, DMAs re-read this block
   const int nb = int(kb1 - kb0);
   const uint16_t* __restrict__ A = static_cast<const uint16_t*>(a.A);
   const uint16_t* __restrict__ Bm = static_cast<const uint16_t*>(a.B);
@@ -251,9 +263,9 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     const uint16_t* p;  // first row of the block (clamped into the range)
     int nv;             // valid rows
   };
-  auto blk = [&](int64_t kb) __attribute__((always_inline)) {
-    const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
-    const int64_t r0 = kc * PRB;
+  auto blk = [&](int kb) __attribute__((always_inline)) {
+    const int kc = kb < kb1 ? kb : kblast;
+    const int64_t r0 = int64_t(kc) * PRB;
     return Blk{A + r0 * lda, int(rows - r0 < PRB ? rows - r0 : PRB)};
   };
   // strip k of a block into a slot: 2 instructions.  Strips wholly past cols load columns
@@ -264,19 +276,17 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       // every strip of every block lies inside the rows: base = the block's first row at c0,
       // strip k at the immediate offset 128 k (k is a constant once the loops are unrolled)
       const uint16_t* base = b.p + c0;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        uint8_t* d = slot + 2048 * k + 1024 * j;
-        switch (k) {
-          case 0: dma_off<0>(base, vf[j], d); break;
-          case 1: dma_off<128>(base, vf[j], d); break;
-          case 2: dma_off<256>(base, vf[j], d); break;
-          case 3: dma_off<384>(base, vf[j], d); break;
-          case 4: dma_off<512>(base, vf[j], d); break;
-          case 5: dma_off<640>(base, vf[j], d); break;
-          case 6: dma_off<768>(base, vf[j], d); break;
-          default: dma_off<896>(base, vf[j], d); break;
-        }
+      const uint32_t v1m = vf[1] - 1024u;
+      uint8_t* d = slot + 2048 * k;
+      switch (k) {
+        case 0: dma_strip_off<0>(base, vf[0], v1m, d); break;
+        case 1: dma_strip_off<128>(base, vf[0], v1m, d); break;
+        case 2: dma_strip_off<256>(base, vf[0], v1m, d); break;
+        case 3: dma_strip_off<384>(base, vf[0], v1m, d); break;
+        case 4: dma_strip_off<512>(base, vf[0], v1m, d); break;
+        case 5: dma_strip_off<640>(base, vf[0], v1m, d); break;
+        case 6: dma_strip_off<768>(base, vf[0], v1m, d); break;
+        default: dma_strip_off<896>(base, vf[0], v1m, d); break;
       }
     } else {
       const int cb = c0 + 64 * k;
@@ -286,7 +296,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       for (int j = 0; j < 2; ++j) dma_row(base, full ? vf[j] : vp[j], slot + 2048 * k + 1024 * j);
     }
   };
-  auto dma = [&](int64_t kb, uint8_t* slot) __attribute__((always_inline)) {
+  auto dma = [&](int kb, uint8_t* slot) __attribute__((always_inline)) {
     const Blk b = blk(kb);
     uint32_t vf[2], vp[2];
     voffs(b.nv, vf, vp);
@@ -300,12 +310,12 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   const int pfd = batch.pfd;
   const uint32_t pfoff = uint32_t(c0 + 64 * (lane & 7) < cols ? c0 + 64 * (lane & 7) : 0) * 2u;
   const uint32_t pfv = uint32_t(lane >> 3) * uint32_t(lda) * 2u + pfoff;  // FULL: lane offset from row 8h
-  auto pf = [&](int64_t kb) __attribute__((always_inline)) {
-    const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
+  auto pf = [&](int kb) __attribute__((always_inline)) {
+    const int kc = kb < kb1 ? kb : kblast;
     if constexpr (FULL) {
-      pf4_s(A + (kc * PRB + 8 * h) * lda, pfv, &sink[w][0]);
+      pf4_s(A + (int64_t(kc) * PRB + 8 * h) * lda, pfv, &sink[w][0]);
     } else {
-      int64_t row = kc * PRB + 8 * h + (lane >> 3);
+      int64_t row = int64_t(kc) * PRB + 8 * h + (lane >> 3);
       row = row < rows ? row : rows - 1;
       pf4(reinterpret_cast<const uint8_t*>(A + row * lda) + pfoff, &sink[w][0]);
     }
@@ -314,14 +324,14 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   // other waves touch the same rows into their sink instead, so every wave counts one load
   const int brow = lane >> 2, bpiece = lane & 3;
   const uint32_t bv = uint32_t(brow * K + 8 * bpiece) * 2u;  // FULL: lane offset from the block's first B row
-  auto dma_b = [&](int64_t kb, uint8_t* bslot) __attribute__((always_inline)) {
-    const int64_t kc = kb < kb1 ? kb : (kb1 > kb0 ? kb1 - 1 : kb0);
+  auto dma_b = [&](int kb, uint8_t* bslot) __attribute__((always_inline)) {
+    const int kc = kb < kb1 ? kb : kblast;
     if constexpr (FULL) {
-      const uint16_t* sb = Bm + kc * PRB * K + PH * h;
+      const uint16_t* sb = Bm + int64_t(kc) * PRB * K + PH * h;
       if (w == 0) dma16_s(sb, bv, bslot);
       else pf4_s(sb, bv, &sink[w][0]);
     } else {
-      int64_t row = kc * PRB + brow;
+      int64_t row = int64_t(kc) * PRB + brow;
       row = row < rows ? row : rows - 1;
       const uint16_t* src = Bm + row * K + PH * h + 8 * bpiece;
       if (w == 0) dma16(src, bslot);
@@ -440,8 +450,8 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     pt[w][1][lane] = p1[1];
     barrier();
     {
-      const int64_t row0 = (kb0 + u) * PRB + 4 * g;
-      const bool ragged = !FULL && (kb0 + u + 1) * PRB > rows;  // wave-uniform
+      const int64_t row0 = int64_t(kb0 + u) * PRB + 4 * g;
+      const bool ragged = !FULL && int64_t(kb0 + u + 1) * PRB > rows;  // wave-uniform
       f32x4 pv[2][QW];  // all eight reads in flight at once
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -459,10 +469,11 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
         uint32_t H[2], L[2];
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
-          const uint16_t h0 = bf16_cvt(v[2 * d]), h1 = bf16_cvt(v[2 * d + 1]);
-          const uint16_t l0 = bf16_cvt(v[2 * d] - bf16_f32(h0)), l1 = bf16_cvt(v[2 * d + 1] - bf16_f32(h1));
-          H[d] = uint32_t(h0) | uint32_t(h1) << 16;
-          L[d] = uint32_t(l0) | uint32_t(l1) << 16;
+          // packed conversions (v_cvt_pk_bf16_f32, round to nearest even): hi of two rows at
+          // once, back to fp32 by a shift / mask, lo of the remainders at once
+          H[d] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2 * d], v[2 * d + 1]}, bf16x2));
+          const float h0 = __uint_as_float(H[d] << 16), h1 = __uint_as_float(H[d] & 0xffff0000u);
+          L[d] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2 * d] - h0, v[2 * d + 1] - h1}, bf16x2));
         }
         uint32_t X[2], Y[2];
 #pragma unroll
@@ -481,7 +492,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     dma_b(kb0 + u + 2, bslot);
     const Blk nb2 = blk(kb0 + u + 2);
     uint32_t vf[2] = {vfull[0], vfull[1]}, vp[2] = {vpart[0], vpart[1]};
-    if (nb2.nv < PRB) voffs(nb2.nv, vf, vp);
+    if (!FULL && nb2.nv < PRB) voffs(nb2.nv, vf, vp);
 #pragma unroll
     for (int c = 0; c < NCT / CH; ++c) {
       if (c == 0) {
@@ -489,6 +500,10 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
         for (int c2 = 1; c2 < P2L; ++c2) rd(c2, tb[c2]);
       }
       if (c + P2L < NCT / CH) rd(c + P2L, tb[(c + P2L) % (P2L + 1)]);
+      // one wait for this chunk's reads (the younger chunks' 8 P2L reads stay in flight)
+      // instead of one per MFMA pair
+      if (c + P2L < NCT / CH) lgkm_wait<2 * CH * P2L>();
+      else lgkm_wait<0>();
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < CH; ++k) {

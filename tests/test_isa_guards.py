@@ -3,7 +3,8 @@
 lsqp4_kernel.hip issues its LDS-DMAs (`global_load_lds_dword[x4]`) from inline asm that loads
 the LDS destination into M0.  Two rules keep that correct without saving M0 around every DMA
 (saving it cost c5 1.5-2.5 %, profiles/r03_dma_asm_ab.txt):
-  * the SALU write of M0 and the DMA reading it are one wait state apart (`s_nop 0`);
+  * the SALU write of M0 and the DMA reading it are one wait state apart (`s_nop 0`); a
+    second DMA of the same asm block (the other half of a strip) reuses that M0;
   * the compiler itself never touches M0 in these kernels, so nothing it emits can see the
     value the asm leaves there (checked here on the generated code, so a compiler or source
     change that starts using M0 fails this test instead of corrupting LDS silently).
@@ -31,13 +32,13 @@ def _asm(tmp_path, src):
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
 def test_lsqp4_m0_writes_are_separated_and_private(tmp_path):
     text = _asm(tmp_path, "lsqp4_kernel.hip")
-    in_asm = False
+    in_asm = m0_in_block = False
     prev = None
     m0_writes = dma = 0
     for raw in text.splitlines():
         line = raw.split(";")[0].strip()
         if raw.strip().startswith(";;#ASMSTART"):
-            in_asm, prev = True, None
+            in_asm, prev, m0_in_block = True, None, False
             continue
         if raw.strip().startswith(";;#ASMEND"):
             in_asm = False
@@ -52,6 +53,12 @@ def test_lsqp4_m0_writes_are_separated_and_private(tmp_path):
             m0_writes += 1
         if line.startswith("global_load_lds"):
             dma += 1
-            assert prev == "s_nop 0", f"LDS-DMA right after the M0 write without a wait state: {prev!r} -> {line}"
+            # the first DMA after an M0 write sits one wait state behind it; further DMAs of
+            # the same asm block (a strip's two halves) reuse that M0 value
+            assert prev == "s_nop 0" or (prev or "").startswith("global_load_lds"), \
+                f"LDS-DMA right after the M0 write without a wait state: {prev!r} -> {line}"
+            assert m0_in_block, f"LDS-DMA in an asm block that did not set M0: {line}"
+        if line.startswith("s_mov_b32 m0,"):
+            m0_in_block = True
         prev = line
-    assert m0_writes > 0 and dma == m0_writes
+    assert m0_writes > 0 and m0_writes <= dma <= 2 * m0_writes

@@ -1,0 +1,19 @@
+# Round 3, session 2: lsqp4 FULL form v2 (a strip's two DMAs under one M0 write, one LDS wait
+# per phase-2 chunk, 32-bit scalar block indices, packed hi/lo conversions) parity, then a
+# same-box c5 A/B against v1 (b017225) and the round-start library (profiles/r03_c5_full_ab.txt)
+set -u
+O=gpurun_out/r03o
+mkdir -p $O
+L=$PWD/mpistragglers.jl_amd
+timeout -k 10 600 python -u -m pytest tests/test_gpu_lsqb.py tests/test_gpu_capi_client.py tests/test_gpu_gated.py -k "lsq or capi or c5 or full" -x -v -rP --timeout 180 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; grep -E "^(FAILED)|passed|failed|FULL worker" $O/tests.log | tail -5; [ $rc -eq 0 ] || exit $rc
+b() {  # label lib
+  MPA_LIB=$2 timeout -k 10 240 python -u bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baseline > $O/$1.log 2>&1 || exit $?
+  grep '^{' $O/$1.log > $O/$1.json
+  echo "$1 $(python3 -c "import json;d=json.load(open('$O/$1.json'));r=d['roofline'];print(d['value'], d['ms_per_step'], r['avg_launch_ms'], r['frac'])")"
+}
+for k in 1 2 3; do
+  b v2_$k $L/_build/libmpiasyncpools.so
+  b v1_$k $L/_build_ab_v1/libmpiasyncpools.so
+  b old$k $L/_build_ab_old/libmpiasyncpools.so
+done
