@@ -82,6 +82,27 @@ static_assert(NKS == 16 && NCT == 32, "8 strips of 64 columns per wave");
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+#ifndef MPA_LSQP4_VACC
+#define MPA_LSQP4_VACC 1  // phase-1 accumulators in VGPRs (inline asm MFMAs)
+#endif
+// Phase 1's accumulators in VGPRs.  G takes all 256 AGPRs, and the compiler gives every MFMA
+// intrinsic AGPR accumulators, so with intrinsics it parks 8 G registers in VGPRs around every
+// phase 1 (24 moves per block).  These asm forms keep the phase-1 chain in VGPRs.  Hazards are
+// the kernel's (the compiler does not look inside): the chain reads its own previous result as
+// SrcC (exact overlap: back to back is allowed), A / B operands come from LDS reads (lgkmcnt,
+// which the compiler does insert for asm operands) or registers written long before; the one
+// non-MFMA reader of the result gets 16 wait states first (mfma_v_settle)
+__device__ __forceinline__ f32x4 mfma_v0(const bf16x8& a, const bf16x8& b) {
+  f32x4 d;
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ void mfma_v(f32x4& d, const bf16x8& a, const bf16x8& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_v_settle(f32x4& d0, f32x4& d1) {
+  asm volatile("s_nop 7\n\ts_nop 7" : "+v"(d0), "+v"(d1));
+}
 __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xc07f); }  // lgkmcnt(0)
 // lgkmcnt(N) alone (vmcnt / expcnt fields left free)
 template <int N>
@@ -164,6 +185,9 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   // may store block u + 1's partial while a slower wave still reads block u's
   __shared__ __attribute__((aligned(16))) f32x4 part[2][QW][2][64];
   __shared__ __attribute__((aligned(16))) uint32_t sink[QW][64];
+  // zeros in B's slot layout, one per wave (each wave zeroes its own: no barrier): the -B MFMA
+  // operand of waves 1-3 (MPA_LSQP4_VACC)
+  __shared__ __attribute__((aligned(16))) uint8_t bzero[QW][PRB * PH * 2];
 
   // blocks b and b + 8 are the two halves of one pair (one XCD under round-robin placement;
   // speed only): pair index = (b / 16) * 8 + b % 8
@@ -234,6 +258,8 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       }
     lgkm_drain();
   }
+  *reinterpret_cast<uint4*>(&bzero[w][16 * lane]) = make_uint4(0, 0, 0, 0);
+  lgkm_drain();
 
   // ---- the wave's DMA of block kb (clamped: past the range it re-reads the range's last
   // block into the free slot, unused, so every step issues the same number of loads)
@@ -397,6 +423,19 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     // of the MFMAs, each strip's after its wait
     constexpr int AD = MPA_LSQP4_AD;
     wait_strip((AD - 1) / 2);  // the strips of the first AD k-steps (and B, older)
+#if MPA_LSQP4_VACC
+    // every wave starts its chain with the B MFMA: wave 0 DMA'd B, and its accumulators start
+    // at -B (A operand: lane (i, g) = row i, iterates 8g .. 8g + 7 of the half, one 16-B read of
+    // the row-major slot, against -I: exact, one nonzero product per output added to 0); the
+    // other waves read a zero slot, so their chains start at 0 with no separate initialisation
+    f32x4 p1[2];
+    {
+      const bf16x8 bfr = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+          (w == 0 ? bslot : &bzero[w][0]) + i * (PH * 2) + 16 * g));
+      p1[0] = mfma_v0(bfr, NEGI[0]);
+      p1[1] = mfma_v0(bfr, NEGI[1]);
+    }
+#else
     f32x4 p1[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     if (w == 0) {
       // wave 0 DMA'd B: its accumulators start at -B, by one MFMA per iterate tile of the B rows
@@ -406,6 +445,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       p1[0] = mfma(bfr, NEGI[0], p1[0]);
       p1[1] = mfma(bfr, NEGI[1], p1[1]);
     }
+#endif
     {
     bf16x8 af[AD];
     auto rd1 = [&](int s) __attribute__((always_inline)) {
@@ -417,11 +457,19 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     for (int s = 0; s < NKS; ++s) {
       __builtin_amdgcn_sched_barrier(0);
       if (s + AD < NKS && ((s + AD) & 1) == 0) wait_strip((s + AD) / 2);
+#if MPA_LSQP4_VACC
+      mfma_v(p1[0], af[s % AD], XF[s][0]);
+      mfma_v(p1[1], af[s % AD], XF[s][1]);
+#else
       p1[0] = mfma(af[s % AD], XF[s][0], p1[0]);
       p1[1] = mfma(af[s % AD], XF[s][1], p1[1]);
+#endif
       if (s + AD < NKS) af[s % AD] = rd1(s + AD);
     }
     __builtin_amdgcn_sched_barrier(0);
+#if MPA_LSQP4_VACC
+    mfma_v_settle(p1[0], p1[1]);
+#endif
     }
     // phase 2's column tiles in chunks of 4 = one strip (8 transposed reads), double-buffered:
     // the reads of chunk c + 1 are issued before the MFMAs of chunk c; chunk 0's go out before
