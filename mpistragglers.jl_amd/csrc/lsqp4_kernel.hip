@@ -82,6 +82,12 @@ static_assert(NKS == 16 && NCT == 32, "8 strips of 64 columns per wave");
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// MPA_LSQP4_PROBE (timing-probe builds only, wrong results: make BUILD=... EXTRA=-DMPA_LSQP4_PROBE=n,
+// profiles/r03_c5_probes.txt): 1 no strip DMAs in the block loop, 2 no cross-wave exchange /
+// barrier in the reduce, 4 no phase-1 MFMAs
+#ifndef MPA_LSQP4_PROBE
+#define MPA_LSQP4_PROBE 0
+#endif
 #ifndef MPA_LSQP4_VACC
 #define MPA_LSQP4_VACC 1  // phase-1 accumulators in VGPRs (inline asm MFMAs)
 #endif
@@ -457,7 +463,9 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     for (int s = 0; s < NKS; ++s) {
       __builtin_amdgcn_sched_barrier(0);
       if (s + AD < NKS && ((s + AD) & 1) == 0) wait_strip((s + AD) / 2);
-#if MPA_LSQP4_VACC
+#if MPA_LSQP4_PROBE & 4
+      (void)af;
+#elif MPA_LSQP4_VACC
       mfma_v(p1[0], af[s % AD], XF[s][0]);
       mfma_v(p1[1], af[s % AD], XF[s][1]);
 #else
@@ -494,17 +502,26 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     // Y = (H2 H3 L2 L3); permlane16 (X, Y) -> X = (H0 H2 L0 L2), Y = (H1 H3 L1 L3) = the first
     // and second four k of every lane group
     bf16x8 RF[2];
+#if MPA_LSQP4_PROBE & 2
+    if (true) {  // timing probe: no cross-wave exchange (own partial only, no barrier)
+      f32x4 pv[2][QW];
+      for (int t = 0; t < 2; ++t)
+        for (int ww = 0; ww < QW; ++ww) pv[t][ww] = p1[t];
+#else
     pt[w][0][lane] = p1[0];
     pt[w][1][lane] = p1[1];
     barrier();
     {
+#endif
       const int64_t row0 = int64_t(kb0 + u) * PRB + 4 * g;
       const bool ragged = !FULL && int64_t(kb0 + u + 1) * PRB > rows;  // wave-uniform
+#if !(MPA_LSQP4_PROBE & 2)
       f32x4 pv[2][QW];  // all eight reads in flight at once
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int ww = 0; ww < QW; ++ww) pv[t][ww] = pt[ww][t][lane];
+#endif
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         f32x4 v = pv[t][0];
@@ -561,7 +578,9 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
         G[1][CH * c + k] = mfma(RF[1], bt, G[1][CH * c + k]);
       }
       __builtin_amdgcn_sched_barrier(0);
+#if !(MPA_LSQP4_PROBE & 1)  // timing probe 1: no strip DMAs in the loop (A stays stale in LDS)
       dma_strip(nb2, vf, vp, c, slot);
+#endif
     }
     pf(kb0 + u + 2 + pfd);
   };
