@@ -88,6 +88,9 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 #ifndef MPA_LSQP4_PROBE
 #define MPA_LSQP4_PROBE 0
 #endif
+#ifndef MPA_LSQP4_P2I
+#define MPA_LSQP4_P2I 1  // phase-2 reads interleaved with the MFMAs
+#endif
 #ifndef MPA_LSQP4_VACC
 #define MPA_LSQP4_VACC 1  // phase-1 accumulators in VGPRs (inline asm MFMAs)
 #endif
@@ -560,6 +563,28 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     if (!FULL && nb2.nv < PRB) voffs(nb2.nv, vf, vp);
 #pragma unroll
     for (int c = 0; c < NCT / CH; ++c) {
+#if MPA_LSQP4_P2I
+      // the reads of chunk c + 1 go out BETWEEN this chunk's MFMAs, one per MFMA gap, instead of
+      // as a cluster of eight before them (one wave per SIMD: clustered issue stretches the gaps)
+      static_assert(P2L == 1, "interleaved phase-2 reads look one chunk ahead");
+      lgkm_wait<0>();  // this chunk's reads, issued during the previous chunk's MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 1 < NCT / CH) rd(c + 1, tb[(c + 1) & 1]);
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const bf16x8 bt = __builtin_bit_cast(
+            bf16x8, __builtin_shufflevector(tb[c & 1][k][0], tb[c & 1][k][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        G[0][CH * c + k] = mfma(RF[0], bt, G[0][CH * c + k]);
+        G[1][CH * c + k] = mfma(RF[1], bt, G[1][CH * c + k]);
+      }
+      if (c + 1 < NCT / CH) {
+#pragma unroll
+        for (int j = 0; j < 2 * CH; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+        }
+      }
+#else
       if (c == 0) {
 #pragma unroll
         for (int c2 = 1; c2 < P2L; ++c2) rd(c2, tb[c2]);
@@ -577,6 +602,7 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
         G[0][CH * c + k] = mfma(RF[0], bt, G[0][CH * c + k]);
         G[1][CH * c + k] = mfma(RF[1], bt, G[1][CH * c + k]);
       }
+#endif
       __builtin_amdgcn_sched_barrier(0);
 #if !(MPA_LSQP4_PROBE & 1)  // timing probe 1: no strip DMAs in the loop (A stays stale in LDS)
       dma_strip(nb2, vf, vp, c, slot);
