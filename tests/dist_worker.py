@@ -255,8 +255,9 @@ def lsq_dist_armed(rank, world, port, placement, delayed, result_q):
         raise
 
 
-def lsqb_dist(rank, world, port, placement, result_q):
-    """The batched 64-iterate variant across processes (pre-armed on the serving rank)."""
+def lsqb_dist(rank, world, port, placement, cols, result_q):
+    """The batched 64-iterate variant across processes (pre-armed on the serving rank); at
+    2048 columns and 1024 rows every task takes lsqp4's FULL form, the armed one included."""
     import numpy as np
     try:
         dist = _init(rank, world, port)
@@ -265,7 +266,7 @@ def lsqb_dist(rank, world, port, placement, result_q):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import mpiasyncpools as M
         import lsq
-        n, rows, cols, K, seed = len(placement), 1000, 256, 64, 29
+        n, rows, K, seed = len(placement), (1024 if cols == 2048 else 1000), 64, 29
         name = [f"/mpa_b{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
         if rank == 0:
             comm = M.DistComm(n, placement, 0, name[0], cols * K * 4, transport="hip")

@@ -54,14 +54,16 @@ def test_lsq_two_processes_prearmed(built, monkeypatch):
     _run(dist_worker.lsq_dist_armed, 2, [0, 1, 1, 1], [4])
 
 
+@pytest.mark.parametrize("cols", [256, 2048])
 @pytest.mark.parametrize("arm", ["0", "2"])
-def test_lsqb_two_processes(built, monkeypatch, arm):
-    """The batched variant across processes, host-launched and device-armed (default)."""
+def test_lsqb_two_processes(built, monkeypatch, arm, cols):
+    """The batched variant across processes, host-launched and device-armed (default); at 2048
+    columns the FULL form of lsqp4, armed (its doorbell-waiting instantiation) and not."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     monkeypatch.setenv("MPA_ARM", arm)
-    _run(dist_worker.lsqb_dist, 2, [0, 1])
+    _run(dist_worker.lsqb_dist, 2, [0, 1], cols)
 
 
 @pytest.mark.parametrize("placement,env", [
