@@ -38,7 +38,9 @@ METRIC = "iterations/sec + shard-kernel HBM GB/s (% peak), nwait=k of 1/2/4/8 GP
 CONFIGS = {
     # the reference's own CPU example restated on the device: coordinator + 3 workers,
     # nwait = 2 (examples/iterative_example.jl structure; latency-bound)
-    "c1": dict(rows=3 << 12, cols=64, workers=3, nwait=2, dtype="f64",
+    # timing_period: one launch in 16 carries the HIP timing events (their host cost sits on
+    # this config's critical path; every launch of the bandwidth-bound configs carries them)
+    "c1": dict(rows=3 << 12, cols=64, workers=3, nwait=2, dtype="f64", timing_period=16,
                desc="BASELINE configs[0] shape: 3 workers, fp64 least squares A 3*2^12 x 64, nwait=2 (latency-bound)"),
     "c2": dict(rows=1 << 20, cols=1024, workers=8, nwait=8, dtype="f32",
                desc="BASELINE configs[1]: fp32 least squares A 2^20x1024 row-sharded over 8 logical workers, "
@@ -68,6 +70,8 @@ def parse():
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--timing-period", type=int, default=None,
+                   help="time one in every k launches with HIP events (default: the config's, 1 or 16 for c1)")
     p.add_argument("--dry-run", action="store_true",
                    help="exercise the launcher, rank placement and max-over-ranks report with no GPU work "
                         "(tests/test_bench_launch.py)")
@@ -234,12 +238,17 @@ def exchange_report(xt):
             "remote_GBps": round(remote / (ms / 1e3) / 1e9, 3) if ms > 0 else None}
 
 
+def timing_period(args, cfg):
+    return args.timing_period if getattr(args, "timing_period", None) else cfg.get("timing_period", 1)
+
+
 def report(args, cfg, world, el, per_rank, extra):
     """per_rank: (launches, summed kernel ms, algorithmic bytes, busy ms) of each GPU.
     roofline.achieved = algorithmic bytes / busy time (the union of the launch intervals, so
     concurrent single-task launches of delayed workers are not double counted), averaged
     over the GPUs; avg_launch_ms = summed kernel ms / launches."""
     its = args.steps / el
+    tp = timing_period(args, cfg)
     n, rows, cols = cfg["workers"], cfg["rows"], cfg["cols"]
     kl = sum(p[0] for p in per_rank)
     kms = sum(p[1] for p in per_rank)
@@ -296,8 +305,10 @@ def report(args, cfg, world, el, per_rank, extra):
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kernel_name(cfg),
                      "alg_bytes_per_launch": per_launch_bytes, "avg_launch_ms": round(per_launch_s * 1e3, 4),
-                     "avg_launch_ms_source": "HIP events recorded around every launch on the stream it runs on "
-                                             "(this run, timed region only); achieved = alg bytes / busy ms",
+                     "avg_launch_ms_source": "HIP events recorded around %s on the stream it runs on "
+                                             "(this run, timed region only); achieved = alg bytes / busy ms" % (
+                                                 "every launch" if tp == 1 else "one in every %d launches" % tp),
+                     "timing_sample_period": tp,
                      "launches": kl, "busy_ms": round(sum(p[3] for p in per_rank), 3)},
         "epoch_alg_GBps": round(epoch_bytes * its / 1e9, 1),
     }
@@ -441,13 +452,17 @@ def run_single(args, cfg):
     torch.cuda.synchronize()
     progress("warmup done (%d epochs)" % args.warmup)
     comm.timing()
-    comm.set_timing(True)
+    comm.set_timing(True, timing_period(args, cfg))
+    steps0 = {k: comm.counter(k) for k in ("head_steps", "epoch_kernels")}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loop(args.steps)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     timing = comm.timing()
+    # where the timed region's epoch steps ran: at the head of the task launch, as their own
+    # epoch kernel (the rest ride in launch tails, launch-ahead at nwait = n)
+    extra["epoch_steps"] = {k: comm.counter(k) - v for k, v in steps0.items()}
     extra["exchange"] = exchange_report(comm.exchange_timing())
     fresh = int((pool.repochs == pool.epoch).sum())
     # launches after the timed region (waitall releases held stale re-dispatches): counted, so
@@ -520,7 +535,7 @@ def run_multi(args, cfg, rank, world, local):
     else:
         comm.serve()  # warmup session, returns at pause_servers
     comm.timing()
-    comm.set_timing(True)
+    comm.set_timing(True, timing_period(args, cfg))
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()

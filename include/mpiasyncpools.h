@@ -218,7 +218,9 @@ int mpa_comm_pause_servers(mpa_comm* comm);
  * mailbox, 2 device memory over xGMI (HIP IPC; MPA_XGMI=0 forces 1) */
 int mpa_comm_payload_path(mpa_comm* comm, int64_t rank);
 /* HIP transport: time every worker-task kernel launch with HIP events on the stream it
- * runs on (enable = 1 / 0).  mpa_comm_timing returns, since its previous call:
+ * runs on (enable = 1 / 0; enable = k > 1 samples one in every k launches, and one in every
+ * k epoch kernels, keeping the events' own host cost off the latency-bound critical path).
+ * mpa_comm_timing returns, since its previous call:
  * out[0] launches, out[1] summed kernel milliseconds, out[2] summed algorithmic bytes
  * (A_i + b_i + x + g_i of every task in the launch), out[3] the
  * milliseconds during which at least one of those launches ran (their union: launches of

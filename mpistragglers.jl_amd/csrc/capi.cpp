@@ -21,7 +21,7 @@ void sim_advance(Comm* c, int64_t dt);
 int64_t sim_now(const Comm* c);
 void hip_set_stream(Comm* c, void* s);
 void* hip_get_stream(Comm* c);
-void hip_set_timing(Comm* c, bool on);
+void hip_set_timing(Comm* c, int period);
 void hip_timing(Comm* c, double out[4]);
 void hip_exchange_timing(Comm* c, double out[3]);
 extern int g_lsq_grid;
@@ -325,7 +325,8 @@ int mpa_comm_set_timing(mpa_comm* comm, int enable) {
   return guarded([&] {
     mpa::Comm& c = comm_of(comm);
     need_hip(c);
-    mpa::hip_set_timing(&c, enable != 0);
+    if (enable < 0) mpa::fail(MPA_ARGUMENT_ERROR, "enable < 0");
+    mpa::hip_set_timing(&c, enable);
   });
 }
 

@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kernels.hpp"
 
 namespace mpa {
@@ -44,11 +46,25 @@ __device__ __forceinline__ void est(T* p, const EVec<T, V>& v) {
     for (int e = 0; e < V; ++e) p[e] = v.v[e];
 }
 
+// relaxed agent-scope element store / load: write-through to the coherence point, visible to
+// workgroups on other XCDs without an L2 writeback / invalidate (the fused head's messages)
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+  using U = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned>::type;
+  __hip_atomic_store(reinterpret_cast<U*>(p), __builtin_bit_cast(U, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  using U = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned>::type;
+  return __builtin_bit_cast(T, __hip_atomic_load(reinterpret_cast<const U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Vectors jv = first, first + stride, ... of V elements (16-B vectors when every pointer
 // allows it).  Every chunk load is issued unconditionally before any arithmetic (chunks past
 // n read x, a valid address, and are ignored): a load under a branch made the compiler wait
 // for each one in turn.
-template <typename T, int V>
+// WT: the dispatch copies are stored write-through (st_agent; the fused head, not bf16 messages)
+template <typename T, int V, bool WT = false>
 __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, int64_t stride) {
   T* recv = reinterpret_cast<T*>(a.recv);
   T* x = static_cast<T*>(a.x);
@@ -92,7 +108,14 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
       if (a.update && a.mirror)
 #pragma unroll
         for (int e = 0; e < V; ++e) a.mirror[j + e] = f32_to_bf16_rne(float(v.v[e]));
-      for (int d = 0; d < a.ndst; ++d) est<T, V>(reinterpret_cast<T*>(a.dst[d]) + j, v);
+      for (int d = 0; d < a.ndst; ++d) {
+        if constexpr (WT) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) st_agent(reinterpret_cast<T*>(a.dst[d]) + j + e, v.v[e]);
+        } else {
+          est<T, V>(reinterpret_cast<T*>(a.dst[d]) + j, v);
+        }
+      }
     }
   }
 }

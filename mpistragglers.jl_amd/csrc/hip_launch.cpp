@@ -357,6 +357,14 @@ void HipComm::launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hip
     }
     b.ep = tail_args_;
     tail_next_ = false;
+  } else if (head_next_) {  // flush: this launch runs this epoch's step first (fused head)
+    if (s != coord_ || ranks.size() != head_ranks_ || batch_armed(b))
+      fail(MPA_ERROR, "fused head: the launch does not cover the epoch's %zu workers", head_ranks_);
+    b.head = epoch_vec(dtype, head_args_) ? 2 : 1;
+    b.head_word = head_word_;
+    b.head_token = ++head_token_;
+    b.ep = head_args_;
+    head_next_ = false;
   }
   enqueue_lsq(b, dtype, int(tasks_[size_t(ranks[0] - 1)].cols), s, bytes);
 }
@@ -671,7 +679,7 @@ HipComm::LsqbLaunch HipComm::build_lsqb_batch(const std::vector<int64_t>& ranks,
 
 void HipComm::enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int64_t armed_rank) {
   TimedLaunch tl{};
-  const bool timed = timing_;
+  const bool timed = sample_task(armed_rank);
   if (timed) {
     std::lock_guard<std::mutex> lk(tm_mu_);
     tl.start = take_event();
@@ -696,7 +704,7 @@ void HipComm::enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int
 
 void HipComm::enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes, int64_t armed_rank) {
   TimedLaunch tl{};
-  const bool timed = timing_;
+  const bool timed = sample_task(armed_rank);
   if (timed) {
     std::lock_guard<std::mutex> lk(tm_mu_);
     tl.start = take_event();

@@ -274,7 +274,7 @@ class HipComm final : public Comm {
   // end_call() leaves the call's harvests pending (they join the next flush's epoch kernel)
   void set_defer_end_flush(bool on) {
     defer_end_ = on;
-    if (!on) tail_next_ = tail_pending_ = false;  // the descent loop ended (or failed)
+    if (!on) tail_next_ = tail_pending_ = head_next_ = false;  // the descent loop ended (or failed)
   }
   void stage_update(const UpdateSpec& u);
   // Launch-ahead (integer nwait == n): the call returns only once all n tasks it posts have
@@ -597,9 +597,18 @@ class HipComm final : public Comm {
 
  public:
   // ---- kernel timing (HIP events around every least-squares launch) ----
-  void set_timing(bool on) {
-    if (!on) reap_timing(true);
-    timing_ = on;
+  // period 0 off; period k >= 1: one in every k launches of each kind is bracketed by events
+  // (armed launches always are: void_timing() cancels the rank's last timed one)
+  void set_timing(int period) {
+    if (period <= 0) {
+      reap_timing(true);
+      timing_ = false;
+      return;
+    }
+    timing_period_ = period;
+    t_seq_ = 0;
+    x_seq_ = 0;
+    timing_ = true;
   }
   // launches, total kernel ms, total algorithmic bytes, and the ms during which at least
   // one timed launch was running (the union of their intervals: concurrent single-task
@@ -672,6 +681,15 @@ class HipComm final : public Comm {
   // profiles/r02_c5_lsqp_tuning.txt
   int lsqp_pfd_ = -1;
   bool tail_next_ = false, tail_pending_ = false;
+  // fused head (flush): the next least-squares launch runs this epoch's step first
+  bool fused_head_ = true;  // MPA_HEAD=0: the step runs as its own epoch kernel
+  bool head_next_ = false;
+  size_t head_ranks_ = 0;
+  EpochArgs head_args_{};
+  uint32_t* head_word_ = nullptr;
+  uint32_t head_token_ = 0;
+  int64_t n_head_ = 0, n_epoch_ = 0;
+  bool head_fits(const std::vector<int64_t>& posted, const UpdateSpec& u) const;
   size_t tail_ranks_ = 0;  // local tasks of the launch that carries the tail
   EpochArgs tail_args_{};
   // rank 0: the completion words of the epoch's remote workers the tail waits for
@@ -694,6 +712,13 @@ class HipComm final : public Comm {
   CallBufs ahead_bufs_;
   bool ahead_update_ = false;
   std::atomic<bool> timing_{false};  // read by the straggler timer thread's launches
+  int timing_period_ = 1;
+  std::atomic<uint64_t> t_seq_{0};  // task launches seen while timing (the timer thread launches too)
+  uint64_t x_seq_ = 0;              // epoch kernels seen while timing
+  bool sample_task(int64_t armed_rank) {
+    if (!timing_) return false;
+    return armed_rank != 0 || timing_period_ <= 1 || t_seq_.fetch_add(1) % uint64_t(timing_period_) == 0;
+  }
   bool debug_ = false;
   int arm_mode_ = 0;
   bool batch_gather_ = true;  // MPA_GATHER=0: a server launches whatever one doorbell scan found
@@ -724,6 +749,7 @@ class HipComm final : public Comm {
   void init_ticket() {
     ticket_ = ctr_ + kLsqCtrPerTask * nworkers_;
     tail_ctr_ = ticket_ + 1;
+    head_word_ = ticket_ + 2;
   }
 };
 

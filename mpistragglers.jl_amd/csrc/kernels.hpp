@@ -146,6 +146,16 @@ struct LsqBatch {
   int tail_nwait;
   const unsigned long long* tail_word[kMaxEpochChunks];
   unsigned long long tail_target[kMaxEpochChunks];
+  // Fused head (the native descent loop at any nwait, every worker of the pool in this launch):
+  // workgroup 0 first runs THIS epoch's coordinator step `ep` (the harvest copies of the
+  // replies the call received, the iterate update, the dispatch copies of this launch's
+  // messages) and publishes head_token in *head_word; every other workgroup waits for it
+  // before it reads its message.  Workgroups are dispatched in order, so workgroup 0 runs
+  // whatever else is resident; the wait is bounded (err bit 128).  head: 0 none, 1 / 2 as
+  // tail; a launch carries a head or a tail, never both.
+  int head;
+  uint32_t* head_word;
+  uint32_t head_token;
   EpochArgs ep;
 };
 static_assert(sizeof(LsqBatch) <= 4096, "LsqBatch is passed by value as kernel arguments (4 KiB)");

@@ -32,6 +32,9 @@
 //               the grid sweeping the task's rows together
 //   M_ARMED     (set per launch, not a tuning bit) every workgroup first waits on the task's
 //               device doorbell (a device-armed task of a worker process, kernels.hpp)
+//   M_HEAD      (set per launch) the fused head: workgroup 0 runs the epoch step first
+//               (LsqBatch::head); a prologue the other launches must not carry (its mere
+//               presence cost the c2 launch 19 %)
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -51,7 +54,7 @@ namespace {
 
 using namespace dev;
 
-enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16, M_BLOCKED = 32, M_ARMED = 64 };
+enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16, M_BLOCKED = 32, M_ARMED = 64, M_HEAD = 128 };
 
 template <typename T, int VPL, int RB, int MODE>
 struct Tile {
@@ -155,7 +158,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     vok[v] = c0 < a.cols;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      xr[v].v[e] = (c0 + e < a.cols) ? xv[c0 + e] : T(0);
+      if constexpr ((MODE & M_HEAD) == 0) xr[v].v[e] = (c0 + e < a.cols) ? xv[c0 + e] : T(0);
       g[v].v[e] = T(0);
     }
   }
@@ -174,9 +177,54 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     base = (int64_t(blk) * kWaves + wave) * RB;
     hi = rows;
   }
+
+  // Fused head: workgroup 0 runs this epoch's coordinator step; its dispatch copies (the
+  // messages the tasks read) are stored write-through, the others' first tile of A is in
+  // flight while they wait for its token, and they read their message write-through too (the
+  // tree's hand-off: no L2 writeback / invalidate).
+  [[maybe_unused]] bool pre = false;
+  Tile<T, VPL, RB, MODE> t0;
+  if constexpr ((MODE & M_HEAD) != 0) {
+    if (blockIdx.x == 0) {
+      if (batch.head == 2) epoch_elems<T, E, true>(batch.ep, tid, kThreads);
+      else epoch_elems<T, 1, true>(batch.ep, tid, kThreads);
+      drain_vm();
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(batch.head_word, batch.head_token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (base < hi) {
+        t0.load(A, base, rows, a.lda, lane, vok);
+        pre = true;
+      }
+      if (tid == 0) {
+        const unsigned long long t0s = rt_now();
+        s_ticket = 1;
+        for (unsigned k = 0;
+             __hip_atomic_load(batch.head_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != batch.head_token; ++k) {
+          __builtin_amdgcn_s_sleep(1);
+          if ((k & 255) == 255 && rt_now() - t0s > batch.spin_ticks) {
+            __hip_atomic_fetch_or(batch.err, 128u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_ticket = 0;  // no work: the host watchdog reports the error word
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      if (!s_ticket) return;
+    }
+  }
+  if constexpr ((MODE & M_HEAD) != 0) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int c0 = (v * 64 + lane) * E;
+#pragma unroll
+      for (int e = 0; e < E; ++e) xr[v].v[e] = (c0 + e < a.cols) ? ld_agent(xv + c0 + e) : T(0);
+    }
+  }
+
   if constexpr (MODE & M_PREFETCH) {
-    Tile<T, VPL, RB, MODE> t0, t1;
-    if (base < hi) t0.load(A, base, rows, a.lda, lane, vok);
+    Tile<T, VPL, RB, MODE> t1;
+    if (base < hi && !pre) t0.load(A, base, rows, a.lda, lane, vok);
     for (;;) {
       const int64_t b1 = base + step;
       if (base >= hi) break;
@@ -187,6 +235,12 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       if (b2 < hi) t0.load(A, b2, rows, a.lda, lane, vok);
       t1.compute(bv, b1, rows, xr, g);
       base = b2;
+    }
+  } else if constexpr ((MODE & M_HEAD) != 0) {
+    for (; base < hi; base += step) {
+      if (!pre) t0.load(A, base, rows, a.lda, lane, vok);
+      pre = false;
+      t0.compute(bv, base, rows, xr, g);
     }
   } else {
     for (; base < hi; base += step) {
@@ -366,6 +420,7 @@ hipError_t go(const LsqBatch& a, hipStream_t s) {
   const int grid = a.block0[a.ntasks];
   if (grid <= 0) return hipSuccess;
   if (batch_armed(a)) hipLaunchKernelGGL((lsq_grad_kernel<T, VPL, RB, MODE | M_ARMED>), dim3(grid), dim3(kThreads), 0, s, a);
+  else if (a.head) hipLaunchKernelGGL((lsq_grad_kernel<T, VPL, RB, MODE | M_HEAD>), dim3(grid), dim3(kThreads), 0, s, a);
   else hipLaunchKernelGGL((lsq_grad_kernel<T, VPL, RB, MODE>), dim3(grid), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }

@@ -56,8 +56,8 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   std::memset(cancel_, 0, sizeof(unsigned long long) * size_t(n + 1));
   xgmi_ = !env_off("MPA_XGMI");
   // per-task tree counters, then the doorbell ticket and the fused-tail counter
-  HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 2)));
-  HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 2)));
+  HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 3)));
+  HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 3)));
   err_dev_ = err_;
   if (region_) {
     if (region_->nworkers() != n) fail(MPA_ARGUMENT_ERROR, "shared memory holds %lld workers, comm has %lld",
@@ -120,6 +120,7 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   const char* cb = measure_env("MPA_COORD_BATCH");
   coord_batches_ = !(cb && *cb == '0');
   fused_tail_ = !env_off("MPA_TAIL");
+  fused_head_ = !env_off("MPA_HEAD");
   { const char* e = measure_env("MPA_LSQP_SHARE"); lsqp_share_ = e && *e == '1'; }
   {
     const char* e = measure_env("MPA_LSQP");  // the product's MPA_LSQP=0 is read where it applies
@@ -282,7 +283,14 @@ void HipComm::flush() {
   }
   if (timing_) reap_timing(false);
   if (has_update_ && fused_ok(upd_, posts_)) {
-    emit_epoch(harv_, harv_before_, posts_, upd_, coord_);
+    if (head_fits(posts_, upd_)) {  // the step runs at the head of the task launch
+      head_args_ = epoch_args(harv_, harv_before_, posts_, upd_);
+      head_next_ = true;
+      head_ranks_ = posts_.size();
+      ++n_head_;
+    } else {
+      emit_epoch(harv_, harv_before_, posts_, upd_, coord_);
+    }
   } else {
     ExchangeBuilder xb(ticket_, &ticket_count_, coord_);
     size_t h0 = 0;
@@ -310,6 +318,7 @@ void HipComm::flush() {
   has_update_ = false;
   harv_.clear();
   launch_local(posts_);
+  if (head_next_) fail(MPA_ERROR, "fused head: no least-squares launch took it");
   posts_.clear();
   maybe_ahead();
 }
@@ -389,7 +398,7 @@ void HipComm::launch_local(const std::vector<int64_t>& posted) {
   // every task of this call is awaited before the caller enqueues anything else on the
   // coordinator stream: run the batch right behind the exchange on that stream (a
   // cross-queue event wait costs ~35 us per epoch, profiles/r01_c2_gaps.json)
-  if (!here.empty()) launch_tasks(here, /*staged=*/false, /*on_coord=*/b_.await_all);
+  if (!here.empty()) launch_tasks(here, /*staged=*/false, /*on_coord=*/b_.await_all || head_next_);
 }
 
 void HipComm::launch_update(const UpdateSpec& u) {
@@ -442,15 +451,35 @@ bool HipComm::tail_fits(const std::vector<int64_t>& posted, const UpdateSpec& u)
   return local >= 1 && local <= size_t(kMaxLsqTasks) && remote <= size_t(kMaxEpochChunks);
 }
 
+// The epoch step rides at the head of the task launch (flush) when that launch is the whole
+// epoch: every worker of the pool posted by this flush, all local undelayed least-squares
+// tasks of one kernel shape, nothing held back.  The launch then runs on the coordinator
+// stream, where the epoch kernel would have run.
+bool HipComm::head_fits(const std::vector<int64_t>& posted, const UpdateSpec& u) const {
+  if (!fused_head_ || int64_t(posted.size()) != b_.n || !held_.empty() || hold_next_ || u.msg_bf16 || u.mirror)
+    return false;
+  int cp = -1;
+  for (int64_t rank : posted) {
+    const HipWorker& w = w_[size_t(rank - 1)];
+    const TaskSpec& ts = tasks_[size_t(rank - 1)];
+    if (w.remote || ts.kind != MPA_TASK_LSQ || !ts.delays_ns.empty() || ts.dtype != u.dtype) return false;
+    const int c = lsq_cols_pad(ts.dtype, int(ts.cols));
+    if (c > kLsqWideSlice || (cp >= 0 && c != cp)) return false;
+    cp = c;
+  }
+  return !posted.empty() && posted.size() <= size_t(kMaxLsqTasks);
+}
+
 void HipComm::emit_epoch(const std::vector<Harvest>& hv, size_t before, const std::vector<int64_t>& posted,
                 const UpdateSpec& u, hipStream_t s) {
   EpochArgs a = epoch_args(hv, before, posted, u);
+  ++n_epoch_;
   if (a.ndoor > 0) {
     a.ticket = ticket_;
     a.ticket_base = ticket_count_;
     ticket_count_ += uint32_t(epoch_grid(u.dtype, a));
   }
-  if (timing_) {
+  if (timing_ && x_seq_++ % uint64_t(timing_period_) == 0) {
     // the exchange this kernel performs over xGMI: messages into remote workers' slots
     // and replies read from their inboxes (mpa_comm_exchange_timing)
     double remote = 0;
@@ -600,6 +629,8 @@ int64_t HipComm::counter(const char* name) const {
   if (k == "held_joined") return n_held_joined_;
   if (k == "held_alone") return n_held_alone_;
   if (k == "gate_steps") return int64_t(gate_steps_taken());
+  if (k == "head_steps") return n_head_;    // epoch steps run at the head of a task launch
+  if (k == "epoch_kernels") return n_epoch_;  // epoch steps run as their own epoch kernel
   return -1;
 }
 
@@ -670,7 +701,7 @@ Comm* make_dist_comm(int64_t nworkers, const int* placement, int my_rank, const 
 
 void hip_set_stream(Comm* c, void* s) { static_cast<HipComm*>(c)->set_stream(static_cast<hipStream_t>(s)); }
 void* hip_get_stream(Comm* c) { return static_cast<HipComm*>(c)->stream(); }
-void hip_set_timing(Comm* c, bool on) { static_cast<HipComm*>(c)->set_timing(on); }
+void hip_set_timing(Comm* c, int period) { static_cast<HipComm*>(c)->set_timing(period); }
 void hip_timing(Comm* c, double out[4]) { static_cast<HipComm*>(c)->timing(out); }
 void hip_exchange_timing(Comm* c, double out[3]) { static_cast<HipComm*>(c)->exchange_timing(out); }
 void hip_serve(Comm* c) { static_cast<HipComm*>(c)->serve(); }

@@ -90,7 +90,7 @@ class _Comm:
 
     def counter(self, name):
         """An event counter of the transport (mpa_comm_counter): "held", "held_joined",
-        "held_alone", "gate_steps"; -1 if the transport does not count it."""
+        "held_alone", "gate_steps", "head_steps", "epoch_kernels"; -1 if the transport does not count it."""
         return int(lib().mpa_comm_counter(self._h, name.encode()))
 
     def set_gate(self, kinds, offsets, ranks):
@@ -169,9 +169,12 @@ class DeviceComm(_Comm):
                                                 C.c_void_p(A.data_ptr()), lda, C.c_void_p(B.data_ptr())))
         self._keep[int(rank)] = (A, B)
 
-    def set_timing(self, enable):
-        """Time every least-squares launch with HIP events on its own stream."""
-        check(lib().mpa_comm_set_timing(self._h, 1 if enable else 0))
+    def set_timing(self, enable, period=1):
+        """Time least-squares launches with HIP events on their own stream: every launch, or
+        one in every `period` launches (and epoch kernels)."""
+        if int(period) < 1:
+            raise ValueError("period must be >= 1")
+        check(lib().mpa_comm_set_timing(self._h, int(period) if enable else 0))
 
     def timing(self):
         """(launches, kernel_ms, algorithmic_bytes, busy_ms) since the previous call;

@@ -316,12 +316,14 @@ def test_full_size_c2_against_torch_fp64(M, torch_mod):
 
 
 @pytest.mark.parametrize("env,cols", [({}, 1024), ({"MPA_TAIL": "0"}, 1024), ({"MPA_AHEAD": "0"}, 1024),
-                                      ({"MPA_FUSE": "0"}, 1024), ({}, 4096)])
+                                      ({"MPA_AHEAD": "0", "MPA_HEAD": "0"}, 1024), ({"MPA_FUSE": "0"}, 1024),
+                                      ({}, 4096)])
 def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod, monkeypatch, env, cols):
     """mpa_lsq_descent makes the same calls as the Python loop: identical iterates (bitwise,
     nwait = n so every epoch is fresh and every kernel is deterministic), with launch-ahead
     and the epoch step fused into the previous launch's tail (default), launch-ahead with a
-    separate epoch kernel, the fused epoch kernel only, and unfused."""
+    separate epoch kernel, no launch-ahead (the step at the head of the task launch, or as
+    its own epoch kernel), and unfused."""
     import lsq
     torch = torch_mod
     for k, v in env.items():
@@ -363,6 +365,92 @@ def test_lsq_descent_native_loop_matches_python_loop(M, torch_mod, monkeypatch, 
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     xs = [xs[0][0], xs[1][0]]
     assert float(torch.linalg.norm(xs[0])) > 0
+
+
+def test_sampled_timing_counts_one_in_k_launches(M, torch_mod, monkeypatch):
+    """mpa_comm_set_timing(comm, k > 1): one in every k task launches and one in every k epoch
+    kernels carry the HIP events (bench.py's latency-bound c1 keeps their host cost off the
+    critical path); the averages stay per timed launch, and 0 turns timing off."""
+    import lsq
+    torch = torch_mod
+    monkeypatch.setenv("MPA_TAIL", "0")
+    monkeypatch.setenv("MPA_AHEAD", "0")
+    monkeypatch.setenv("MPA_HEAD", "0")  # every epoch step its own (timed) epoch kernel
+    n, rows, cols, seed = 3, 1024, 64, 5
+    A = _dev(torch, lsq.gen_matrix(seed, 0, n * rows, cols, "f64"))
+    b = _dev(torch, lsq.gen_vector(seed, 0, n * rows, "f64"))
+    comm = M.DeviceComm(n)
+    for r in range(1, n + 1):
+        comm.set_task_lsq(r, A[(r - 1) * rows:r * rows], b[(r - 1) * rows:r * rows])
+    pool = M.MPIAsyncPool(n)
+    x = torch.zeros(cols, dtype=torch.float64, device="cuda")
+    isend = torch.zeros(n * cols, dtype=torch.float64, device="cuda")
+    recv = torch.zeros_like(isend)
+    irecv = torch.zeros_like(isend)
+    counts = {}
+    for period in (1, 4):
+        comm.timing()
+        comm.exchange_timing()
+        comm.set_timing(True, period)
+        M.lsq_descent(pool, comm, x, recv, isend, irecv, n, 0.01, 8)
+        torch.cuda.synchronize()
+        t = comm.timing()
+        xl = comm.exchange_timing()[0]
+        comm.set_timing(False)
+        assert t[1] > 0 and t[2] > 0 and t[3] > 0
+        counts[period] = (t[0], xl)
+    tasks1, epochs1 = counts[1]
+    assert epochs1 >= 8 and tasks1 >= 8
+    assert counts[4] == ((tasks1 + 3) // 4, (epochs1 + 3) // 4), counts
+    with pytest.raises(ValueError):
+        comm.set_timing(True, 0)
+    comm.close()
+
+
+@pytest.mark.parametrize("dtype,cols", [("f64", 64), ("f32", 1024)])
+def test_fused_head_matches_epoch_kernel(M, torch_mod, monkeypatch, dtype, cols):
+    """The epoch step at the head of the task launch (flush, every worker posted: c1's loop)
+    gives the same iterates, replies and messages bit for bit as the step in its own epoch
+    kernel (MPA_HEAD=0), and it is the one that ran (the transport's counters); nwait < n
+    runs it too, with the pool's bookkeeping intact."""
+    import lsq
+    torch = torch_mod
+    monkeypatch.setenv("MPA_AHEAD", "0")
+    n, rows, seed, epochs = 3, 4096, 11, 12
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+    A = _dev(torch, lsq.gen_matrix(seed, 0, n * rows, cols, dtype))
+    b = _dev(torch, lsq.gen_vector(seed, 0, n * rows, dtype))
+
+    def run(head, nwait):
+        monkeypatch.setenv("MPA_HEAD", "1" if head else "0")
+        comm = M.DeviceComm(n)
+        for r in range(1, n + 1):
+            comm.set_task_lsq(r, A[(r - 1) * rows:r * rows], b[(r - 1) * rows:r * rows])
+        pool = M.MPIAsyncPool(n)
+        x = torch.zeros(cols, dtype=tdt, device="cuda")
+        isend = torch.zeros(n * cols, dtype=tdt, device="cuda")
+        recv = torch.zeros(n * cols, dtype=tdt, device="cuda")
+        irecv = torch.zeros_like(recv)
+        h0, e0 = comm.counter("head_steps"), comm.counter("epoch_kernels")
+        M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, 1e-3, epochs)
+        torch.cuda.synchronize()
+        steps = (comm.counter("head_steps") - h0, comm.counter("epoch_kernels") - e0)
+        M.waitall_(pool, recv, irecv)
+        torch.cuda.synchronize()
+        out = (x.clone(), recv.clone(), isend.clone(), pool.epoch, list(pool.repochs))
+        comm.close()
+        return out, steps
+
+    on, s_on = run(True, n)
+    off, s_off = run(False, n)
+    assert s_on[0] >= epochs - 1 and s_off[0] == 0 and s_off[1] >= epochs - 1, (s_on, s_off)
+    for a, c in zip(on[:3], off[:3]):
+        assert torch.equal(a, c)
+    assert on[3:] == off[3:]
+    assert float(torch.linalg.norm(on[0])) > 0
+    part, s_part = run(True, n - 1)
+    assert s_part[0] >= 1 and part[3] == epochs and max(part[4]) == epochs
+    assert bool(torch.isfinite(part[0]).all()) and float(torch.linalg.norm(part[0])) > 0
 
 
 def test_read_bandwidth_probe(M, torch_mod):
