@@ -453,7 +453,7 @@ def run_single(args, cfg):
     progress("warmup done (%d epochs)" % args.warmup)
     comm.timing()
     comm.set_timing(True, timing_period(args, cfg))
-    steps0 = {k: comm.counter(k) for k in ("head_steps", "epoch_kernels")}
+    steps0 = {k: comm.counter(k) for k in ("head_steps", "epoch_kernels", "prearmed", "prearm_cancelled")}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loop(args.steps)

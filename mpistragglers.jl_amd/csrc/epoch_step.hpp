@@ -4,7 +4,8 @@
 // epoch of the native descent loop at nwait = n is one launch).
 //
 // Per element j of the iterate, in the reference's order: the pending harvest copies
-// `recvbufs[i] .= irecvbufs[i]` (src/MPIAsyncPools.jl:167), the iterate update
+// `recvbufs[i] .= irecvbufs[i]` (src/MPIAsyncPools.jl:167), the messages of held stale
+// re-dispatches (:180-182, the iterate before this update), the iterate update
 // x -= eta * sum_i w_i chunk_i (examples/iterative_example.jl:41-46, the fp64 sum of
 // aggregate_kernel in chunk order, explicit fmas), the harvests that follow the update, and
 // the dispatch copies `isendbufs[i] .= sendbuf` (:130).
@@ -81,6 +82,17 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
 #pragma unroll
     for (int i = 0; i < kMaxEpochChunks; ++i)
       if (i < a.n && a.hsrc[i]) est<T, V>(recv + int64_t(i) * a.elems + j, c[i]);
+    for (int d = 0; d < a.ndst0; ++d) {  // held re-dispatches: the message before the update
+      if (a.msg_bf16) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) reinterpret_cast<uint16_t*>(a.dst0[d])[j + e] = a.mirror[j + e];
+      } else if constexpr (WT) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) st_agent(reinterpret_cast<T*>(a.dst0[d]) + j + e, v.v[e]);
+      } else {
+        est<T, V>(reinterpret_cast<T*>(a.dst0[d]) + j, v);
+      }
+    }
     if (a.update) {
 #pragma unroll
       for (int e = 0; e < V; ++e) {

@@ -362,7 +362,7 @@ void HipComm::launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hip
       fail(MPA_ERROR, "fused head: the launch does not cover the epoch's %zu workers", head_ranks_);
     b.head = epoch_vec(dtype, head_args_) ? 2 : 1;
     b.head_word = head_word_;
-    b.head_token = ++head_token_;
+    b.head_token = next_head_token();
     b.ep = head_args_;
     head_next_ = false;
   }
@@ -702,9 +702,16 @@ void HipComm::enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int
   }
 }
 
-void HipComm::enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes, int64_t armed_rank) {
+void HipComm::enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes, int64_t armed_rank,
+                          bool untimed) {
   TimedLaunch tl{};
-  const bool timed = sample_task(armed_rank);
+  // a pre-armed launch is never timed (it waits for the host inside); the launch pre-arming
+  // skipped for the timing's sake always is
+  bool timed = false;
+  if (!untimed) {
+    timed = time_next_ ? timing_.load() : sample_task(armed_rank);
+    time_next_ = false;
+  }
   if (timed) {
     std::lock_guard<std::mutex> lk(tm_mu_);
     tl.start = take_event();

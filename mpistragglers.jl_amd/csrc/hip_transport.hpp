@@ -273,6 +273,7 @@ class HipComm final : public Comm {
   }
   // end_call() leaves the call's harvests pending (they join the next flush's epoch kernel)
   void set_defer_end_flush(bool on) {
+    if (!on) cancel_pre();
     defer_end_ = on;
     if (!on) tail_next_ = tail_pending_ = head_next_ = false;  // the descent loop ended (or failed)
   }
@@ -593,7 +594,8 @@ class HipComm final : public Comm {
   void enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int64_t armed_rank = 0);
 
   // enqueue one least-squares launch on `s` (coordinator / server thread or timer thread)
-  void enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes, int64_t armed_rank = 0);
+  void enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes, int64_t armed_rank = 0,
+                   bool untimed = false);
 
  public:
   // ---- kernel timing (HIP events around every least-squares launch) ----
@@ -690,6 +692,68 @@ class HipComm final : public Comm {
   uint32_t head_token_ = 0;
   int64_t n_head_ = 0, n_epoch_ = 0;
   bool head_fits(const std::vector<int64_t>& posted, const UpdateSpec& u) const;
+  uint32_t next_head_token() {
+    head_token_ = (head_token_ + 1) & ~kHeadCancel;
+    if (head_token_ == 0) head_token_ = 1;
+    return head_token_;
+  }
+  // Pre-armed launches (the native descent loop at nwait < n, every epoch a fused-head launch
+  // of the whole pool: c1): right after an epoch's launch the next one is enqueued behind it,
+  // its tasks numbered one ahead, its workgroup 0 waiting on a pinned mailbox; the next flush
+  // that posts the same workers writes the epoch step's arguments there and releases it
+  // (pre_consume), anything else cancels it first (cancel_pre).  The host's launch call and
+  // the command processor's dispatch leave the epoch's critical path (7.9 vs 2.8 us round
+  // trip, profiles/r03_launch_cost.txt).  MPA_PREARM=0: off.
+  struct PreMailbox {
+    unsigned long long go;
+    unsigned long long pad[7];
+    EpochArgs ep;
+  };
+  bool prearm_ = true;
+  bool pre_active_ = false;
+  bool pre_vec_ = false;
+  PreMailbox* pre_mb_ = nullptr;  // host-pinned, coherent
+  unsigned long long pre_token_ = 0;
+  std::vector<int64_t> pre_ranks_, last_head_ranks_;
+  std::vector<uint64_t> pre_seq_;
+  std::vector<const uint8_t*> pre_x_;
+  std::vector<uint8_t*> pre_out_;
+  int64_t n_prearmed_ = 0, n_pre_cancel_ = 0, pre_count_ = 0;
+  bool time_next_ = false;  // the next normal launch is timed (pre-arming skipped for it)
+  bool pre_consume();
+  void maybe_prearm(int dtype);
+  // Held stale re-dispatches in the descent loop (flush_stale): their message copies (and the
+  // call's pending harvests) join the next flush's epoch step, before its update (EpochArgs
+  // dst0), instead of an exchange launch of their own; run_deferred() issues them as that
+  // launch when something else must run first (a held task released, a step that cannot
+  // carry them).  {message source, slot, bytes}
+  struct Deferred0 {
+    const uint8_t* src;
+    uint8_t* dst;
+    size_t bytes;
+  };
+  std::vector<Deferred0> stale_deferred_;
+  int64_t n_deferred_ = 0;
+  bool defer_ok_ = true;  // MPA_DEFER=0: a held re-dispatch's copies go out at once
+  bool defer_stale();
+  void run_deferred();
+  bool deferred_fit(const UpdateSpec& u) const {
+    const uint8_t* msg = u.msg_bf16 ? reinterpret_cast<const uint8_t*>(u.mirror) : static_cast<const uint8_t*>(u.x);
+    for (const auto& d : stale_deferred_)
+      if (d.src != msg || d.bytes != b_.sl) return false;
+    return true;
+  }
+  std::vector<int64_t> launch_ranks() const {  // the ranks launch_local would launch together
+    std::vector<int64_t> r(held_);
+    r.insert(r.end(), posts_.begin(), posts_.end());
+    return r;
+  }
+  void cancel_pre() {
+    if (!pre_active_) return;
+    __atomic_store_n(&pre_mb_->go, pre_token_ | kPreCancel, __ATOMIC_RELEASE);
+    pre_active_ = false;
+    ++n_pre_cancel_;
+  }
   size_t tail_ranks_ = 0;  // local tasks of the launch that carries the tail
   EpochArgs tail_args_{};
   // rank 0: the completion words of the epoch's remote workers the tail waits for

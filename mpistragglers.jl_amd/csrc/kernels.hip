@@ -275,9 +275,12 @@ bool epoch_vec(int dtype, const EpochArgs& a) {
   if (a.msg_bf16 || a.mirror) {
     m |= reinterpret_cast<uintptr_t>(a.mirror) & 7u;  // 4 bf16 per thread (8 B)
     for (int d = 0; d < a.ndst; ++d) m |= reinterpret_cast<uintptr_t>(a.dst[d]) & 7u;
+    for (int d = 0; d < a.ndst0; ++d) m |= reinterpret_cast<uintptr_t>(a.dst0[d]) & 7u;
   }
-  if (!a.msg_bf16)
+  if (!a.msg_bf16) {
     for (int d = 0; d < a.ndst; ++d) m |= reinterpret_cast<uintptr_t>(a.dst[d]);
+    for (int d = 0; d < a.ndst0; ++d) m |= reinterpret_cast<uintptr_t>(a.dst0[d]);
+  }
   return a.elems % V == 0 && (m & 15u) == 0;
 }
 

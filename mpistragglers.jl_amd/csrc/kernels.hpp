@@ -64,6 +64,7 @@ struct Publish {
 // every message is handled by one thread, so the stages need no grid-wide ordering.
 constexpr int kMaxEpochChunks = 16;
 constexpr int kMaxEpochDst = 32;
+constexpr int kMaxEpochDst0 = 8;
 struct EpochArgs {
   int64_t elems;  // elements per chunk (T) = per message
   int n;          // chunks of recvbuf
@@ -79,6 +80,10 @@ struct EpochArgs {
   int ndst;
   uint8_t* dst[kMaxEpochDst];
   int ndoor;
+  // dispatch copies of the iterate as it stands BEFORE the update: the stale re-dispatches
+  // held by the previous call's wait (flush_stale deferred their messages into this step)
+  int ndst0;
+  uint8_t* dst0[kMaxEpochDst0];
   unsigned long long* door[kMaxDoorbells];
   unsigned long long doorval[kMaxDoorbells];
   uint32_t* ticket;
@@ -126,6 +131,9 @@ constexpr int kLsqCtrPerTask = 160;  // 128 + 16 + 2 + 1, rounded up
 // Several workers dispatched by the same flush run as ONE launch: workgroups
 // [block0[t], block0[t+1]) belong to task t.  All tasks share (dtype, cols_pad).
 constexpr int kMaxLsqTasks = 16;
+constexpr int kHeadPrearmed = 4;
+constexpr uint32_t kHeadCancel = 0x80000000u;
+constexpr unsigned long long kPreCancel = 1ull << 63;
 struct LsqBatch {
   int ntasks;
   unsigned* err;
@@ -153,9 +161,17 @@ struct LsqBatch {
   // before it reads its message.  Workgroups are dispatched in order, so workgroup 0 runs
   // whatever else is resident; the wait is bounded (err bit 128).  head: 0 none, 1 / 2 as
   // tail; a launch carries a head or a tail, never both.
+  //   head | kHeadPrearmed: a PRE-ARMED launch, enqueued one epoch early (transport_hip.cpp,
+  //   maybe_prearm): workgroup 0 first waits for the host to decide the epoch -- *pre_go (a
+  //   host-pinned word) reaching pre_token -- and reads the step's EpochArgs from *pre_ep (the
+  //   same pinned mailbox) instead of `ep`; pre_token | kPreCancel cancels the launch (every
+  //   workgroup returns, nothing is published).  Bounded like the other waits (err bit 128).
   int head;
   uint32_t* head_word;
-  uint32_t head_token;
+  uint32_t head_token;  // below kHeadCancel; head_token | kHeadCancel: the launch was cancelled
+  const unsigned long long* pre_go;
+  const EpochArgs* pre_ep;
+  unsigned long long pre_token;
   EpochArgs ep;
 };
 static_assert(sizeof(LsqBatch) <= 4096, "LsqBatch is passed by value as kernel arguments (4 KiB)");

@@ -186,8 +186,49 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   Tile<T, VPL, RB, MODE> t0;
   if constexpr ((MODE & M_HEAD) != 0) {
     if (blockIdx.x == 0) {
-      if (batch.head == 2) epoch_elems<T, E, true>(batch.ep, tid, kThreads);
-      else epoch_elems<T, 1, true>(batch.ep, tid, kThreads);
+      // (the step reads its arguments from the kernel arguments or from LDS in two separate
+      // calls: one pointer that may point at either made the compiler copy the 976-B kernarg
+      // EpochArgs to scratch, 3.5 KiB of it per workgroup and 50 us per launch)
+      if (batch.head & kHeadPrearmed) {
+        // pre-armed: the host decides this epoch while the launch waits here; the step's
+        // arguments then come from the pinned mailbox (one pass of 16-B reads into LDS)
+        __shared__ EpochArgs s_ep;
+        __shared__ int s_go;
+        if (tid == 0) {
+          const unsigned long long t0s = rt_now();
+          int go = 1;
+          unsigned long long v;
+          for (unsigned k = 0; ((v = __hip_atomic_load(batch.pre_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) &
+                                ~kPreCancel) != batch.pre_token;
+               ++k) {
+            if ((k & 255) == 255 && rt_now() - t0s > batch.spin_ticks) {
+              __hip_atomic_fetch_or(batch.err, 128u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              v = kPreCancel;
+              break;
+            }
+          }
+          if (v & kPreCancel) go = 0;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the mailbox the host wrote
+          s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) {
+          if (tid == 0)
+            __hip_atomic_store(batch.head_word, batch.head_token | kHeadCancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return;
+        }
+        constexpr int kEpVecs = int(sizeof(EpochArgs) / 16);
+        static_assert(sizeof(EpochArgs) % 16 == 0, "EpochArgs copies in 16-B vectors");
+        for (int k = tid; k < kEpVecs; k += kThreads)
+          reinterpret_cast<uint4*>(&s_ep)[k] = reinterpret_cast<const uint4*>(batch.pre_ep)[k];
+        __syncthreads();
+        if ((batch.head & 3) == 2) epoch_elems<T, E, true>(s_ep, tid, kThreads);
+        else epoch_elems<T, 1, true>(s_ep, tid, kThreads);
+      } else if ((batch.head & 3) == 2) {
+        epoch_elems<T, E, true>(batch.ep, tid, kThreads);
+      } else {
+        epoch_elems<T, 1, true>(batch.ep, tid, kThreads);
+      }
       drain_vm();
       __syncthreads();
       if (tid == 0) __hip_atomic_store(batch.head_word, batch.head_token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -199,10 +240,17 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       if (tid == 0) {
         const unsigned long long t0s = rt_now();
         s_ticket = 1;
-        for (unsigned k = 0;
-             __hip_atomic_load(batch.head_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != batch.head_token; ++k) {
+        // a pre-armed launch waits for the host's decision first: no time bound of its own
+        // here beyond workgroup 0's (which publishes the cancel token on its timeout)
+        for (unsigned k = 0;; ++k) {
+          const uint32_t hw = __hip_atomic_load(batch.head_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (hw == batch.head_token) break;
+          if (hw == (batch.head_token | kHeadCancel)) {
+            s_ticket = 0;
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
-          if ((k & 255) == 255 && rt_now() - t0s > batch.spin_ticks) {
+          if ((k & 255) == 255 && rt_now() - t0s > 2 * batch.spin_ticks) {
             __hip_atomic_fetch_or(batch.err, 128u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             s_ticket = 0;  // no work: the host watchdog reports the error word
             break;

@@ -121,6 +121,10 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   coord_batches_ = !(cb && *cb == '0');
   fused_tail_ = !env_off("MPA_TAIL");
   fused_head_ = !env_off("MPA_HEAD");
+  prearm_ = fused_head_ && !env_off("MPA_PREARM");
+  defer_ok_ = !env_off("MPA_DEFER");
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&pre_mb_), sizeof(PreMailbox), hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset(static_cast<void*>(pre_mb_), 0, sizeof(PreMailbox));
   { const char* e = measure_env("MPA_LSQP_SHARE"); lsqp_share_ = e && *e == '1'; }
   {
     const char* e = measure_env("MPA_LSQP");  // the product's MPA_LSQP=0 is read where it applies
@@ -182,6 +186,11 @@ HipComm::~HipComm() {
   if (flags_) (void)hipHostFree(flags_);
   if (err_) (void)hipHostFree(err_);
   if (cancel_) (void)hipHostFree(cancel_);
+  if (pre_mb_) {
+    cancel_pre();
+    (void)hipStreamSynchronize(coord_);  // the cancelled launch has left before its mailbox goes
+    (void)hipHostFree(pre_mb_);
+  }
   if (xfer_ev_) (void)hipEventDestroy(xfer_ev_);
   delete region_;
 }
@@ -265,6 +274,7 @@ int64_t HipComm::waitany(int64_t n, const int64_t* ranks, const uint8_t* live) {
 }
 
 void HipComm::waitall(int64_t n, const int64_t* ranks, const uint8_t* live) {
+  cancel_pre();
   release_held();
   const auto t0 = Clock::now();
   for (int64_t i = 0; i < n; ++i) {
@@ -277,6 +287,10 @@ void HipComm::waitall(int64_t n, const int64_t* ranks, const uint8_t* live) {
 }
 
 void HipComm::flush() {
+  if (pre_active_ && pre_consume()) return;  // the pre-armed launch runs this epoch
+  if (defer_stale()) return;                 // held re-dispatches: nothing to launch yet
+  cancel_pre();
+  if (!stale_deferred_.empty() && (!has_update_ || !fused_ok(upd_, posts_) || !deferred_fit(upd_))) run_deferred();
   if (posts_.empty() && harv_.empty() && !has_update_) {
     maybe_ahead();
     return;
@@ -286,11 +300,13 @@ void HipComm::flush() {
     if (head_fits(posts_, upd_)) {  // the step runs at the head of the task launch
       head_args_ = epoch_args(harv_, harv_before_, posts_, upd_);
       head_next_ = true;
-      head_ranks_ = posts_.size();
+      last_head_ranks_ = launch_ranks();
+      head_ranks_ = last_head_ranks_.size();
       ++n_head_;
     } else {
       emit_epoch(harv_, harv_before_, posts_, upd_, coord_);
     }
+    stale_deferred_.clear();  // the step carried them
   } else {
     ExchangeBuilder xb(ticket_, &ticket_count_, coord_);
     size_t h0 = 0;
@@ -317,13 +333,88 @@ void HipComm::flush() {
   }
   has_update_ = false;
   harv_.clear();
+  const bool headed = !last_head_ranks_.empty();
+  const int hdtype = upd_.dtype;
   launch_local(posts_);
   if (head_next_) fail(MPA_ERROR, "fused head: no least-squares launch took it");
   posts_.clear();
   maybe_ahead();
+  if (headed) maybe_prearm(hdtype);
+  last_head_ranks_.clear();
+}
+
+// The next epoch, enqueued now behind this one (pre-armed): only in the descent loop at
+// nwait < n (launch-ahead and the fused tail cover nwait = n), right after a fused-head launch
+// of the whole pool, and not for the one launch in `timing_period_` that the timing samples.
+void HipComm::maybe_prearm(int dtype) {
+  if (!prearm_ || !defer_end_ || b_.await_all || gated() || role_ != SOLO || pre_active_ || !held_.empty()) return;
+  if (timing_ && timing_period_ > 1 && ++pre_count_ % timing_period_ == 0) {
+    time_next_ = true;
+    return;
+  }
+  if (timing_ && timing_period_ <= 1) return;  // every launch timed: none pre-armed
+  const std::vector<int64_t>& ranks = last_head_ranks_;
+  for (int64_t rank : ranks) w_[size_t(rank - 1)].seq += 1;  // the tasks of the next epoch
+  double bytes = 0;
+  LsqBatch b = build_lsq_batch(ranks, dtype, &bytes);
+  pre_seq_.clear();
+  pre_x_.clear();
+  pre_out_.clear();
+  for (int64_t rank : ranks) {
+    HipWorker& w = w_[size_t(rank - 1)];
+    pre_seq_.push_back(w.seq);
+    pre_x_.push_back(w.x);
+    pre_out_.push_back(w.out);
+    w.seq -= 1;
+  }
+  pre_vec_ = epoch_vec(dtype, head_args_);
+  b.head = (pre_vec_ ? 2 : 1) | kHeadPrearmed;
+  b.head_word = head_word_;
+  b.head_token = next_head_token();
+  b.pre_go = &pre_mb_->go;
+  b.pre_ep = &pre_mb_->ep;
+  b.pre_token = ++pre_token_;
+  pre_ranks_ = ranks;
+  pre_active_ = true;
+  enqueue_lsq(b, dtype, int(tasks_[size_t(ranks[0] - 1)].cols), coord_, bytes, 0, /*untimed=*/true);
+}
+
+// This flush is the epoch the pre-armed launch was enqueued for: the same workers posted to
+// the same slots with the task numbers it carries, a fused-head step.  Its arguments go to
+// the mailbox, then the go word (release: the launch reads them after it).
+bool HipComm::pre_consume() {
+  const std::vector<int64_t> ranks = launch_ranks();
+  if (!has_update_ || ranks != pre_ranks_ || hold_next_ || !fused_ok(upd_, posts_) || !head_fits(posts_, upd_) ||
+      !deferred_fit(upd_))
+    return false;
+  for (size_t k = 0; k < ranks.size(); ++k) {
+    const HipWorker& w = w_[size_t(ranks[k] - 1)];
+    if (w.seq != pre_seq_[k] || w.x != pre_x_[k] || w.out != pre_out_[k]) return false;
+  }
+  EpochArgs ea = epoch_args(harv_, harv_before_, posts_, upd_);
+  if (ea.ndoor != 0 || epoch_vec(upd_.dtype, ea) != pre_vec_) return false;
+  std::memcpy(static_cast<void*>(&pre_mb_->ep), &ea, sizeof ea);
+  __atomic_store_n(&pre_mb_->go, pre_token_, __ATOMIC_RELEASE);
+  pre_active_ = false;
+  head_args_ = ea;
+  ++n_head_;
+  ++n_prearmed_;
+  const int dtype = upd_.dtype;
+  has_update_ = false;
+  harv_.clear();
+  stale_deferred_.clear();
+  n_held_joined_ += int64_t(held_.size());
+  held_.clear();
+  last_head_ranks_ = ranks;
+  posts_.clear();
+  maybe_prearm(dtype);
+  last_head_ranks_.clear();
+  return true;
 }
 
 void HipComm::release_held() {
+  cancel_pre();
+  run_deferred();  // their messages first
   if (held_.empty()) return;
   std::vector<int64_t> h;
   h.swap(held_);
@@ -345,6 +436,7 @@ void HipComm::stage_update(const UpdateSpec& u) {
 }
 
 void HipComm::shutdown() {
+  cancel_pre();
   gate_off();
   release_held();
   if (role_ != SERVER) {
@@ -366,6 +458,7 @@ void HipComm::shutdown() {
 }
 
 void HipComm::on_task_changed(int64_t rank) {
+  cancel_pre();
   HipWorker& w = w_[size_t(rank - 1)];
   if (!w.here)
     fail(MPA_ARGUMENT_ERROR, "worker %lld is served by another process; register its task there", (long long)rank);
@@ -456,10 +549,11 @@ bool HipComm::tail_fits(const std::vector<int64_t>& posted, const UpdateSpec& u)
 // tasks of one kernel shape, nothing held back.  The launch then runs on the coordinator
 // stream, where the epoch kernel would have run.
 bool HipComm::head_fits(const std::vector<int64_t>& posted, const UpdateSpec& u) const {
-  if (!fused_head_ || int64_t(posted.size()) != b_.n || !held_.empty() || hold_next_ || u.msg_bf16 || u.mirror)
+  // the launch is the held re-dispatches (which join it) and this flush's posts
+  if (!fused_head_ || int64_t(posted.size() + held_.size()) != b_.n || hold_next_ || u.msg_bf16 || u.mirror)
     return false;
   int cp = -1;
-  for (int64_t rank : posted) {
+  for (int64_t rank : launch_ranks()) {
     const HipWorker& w = w_[size_t(rank - 1)];
     const TaskSpec& ts = tasks_[size_t(rank - 1)];
     if (w.remote || ts.kind != MPA_TASK_LSQ || !ts.delays_ns.empty() || ts.dtype != u.dtype) return false;
@@ -467,7 +561,39 @@ bool HipComm::head_fits(const std::vector<int64_t>& posted, const UpdateSpec& u)
     if (c > kLsqWideSlice || (cp >= 0 && c != cp)) return false;
     cp = c;
   }
-  return !posted.empty() && posted.size() <= size_t(kMaxLsqTasks);
+  return !posted.empty() && posted.size() + held_.size() <= size_t(kMaxLsqTasks);
+}
+
+// flush_stale() in the descent loop: every re-dispatch of this flush is held, so nothing needs
+// to run now -- the pending harvests (the stale reply among them) and the held workers'
+// messages go into the next step, ahead of its update, as this flush would have ordered them.
+bool HipComm::defer_stale() {
+  if (!hold_next_ || !defer_end_ || has_update_ || posts_.empty() || !defer_ok_ ||
+      stale_deferred_.size() + posts_.size() > size_t(kMaxEpochDst0))
+    return false;
+  for (int64_t rank : posts_) {
+    const HipWorker& w = w_[size_t(rank - 1)];
+    const TaskSpec& ts = tasks_[size_t(rank - 1)];
+    if (w.remote || (ts.kind != MPA_TASK_LSQ && ts.kind != MPA_TASK_LSQ_BATCH) || !ts.delays_ns.empty()) return false;
+  }
+  for (int64_t rank : posts_) stale_deferred_.push_back({b_.sendbuf, const_cast<uint8_t*>(w_[size_t(rank - 1)].x), b_.sl});
+  launch_local(posts_);  // every one of them is held (hold_next_)
+  n_deferred_ += int64_t(posts_.size());
+  posts_.clear();
+  return true;
+}
+
+void HipComm::run_deferred() {
+  if (stale_deferred_.empty()) return;
+  cancel_pre();
+  ExchangeBuilder xb(ticket_, &ticket_count_, coord_);
+  const size_t nb = has_update_ ? harv_before_ : harv_.size();  // harvests due before the update
+  for (size_t k = 0; k < nb; ++k) add_harvest(xb, harv_[k]);
+  for (const auto& d : stale_deferred_) xb.copy(d.src, d.dst, d.bytes);
+  xb.launch();
+  harv_.erase(harv_.begin(), harv_.begin() + std::ptrdiff_t(nb));
+  if (has_update_) harv_before_ = 0;
+  stale_deferred_.clear();
 }
 
 void HipComm::emit_epoch(const std::vector<Harvest>& hv, size_t before, const std::vector<int64_t>& posted,
@@ -521,6 +647,7 @@ EpochArgs HipComm::epoch_args(const std::vector<Harvest>& hv, size_t before, con
   a.x = u.x;
   a.mirror = u.mirror;
   a.msg_bf16 = u.msg_bf16 ? 1 : 0;
+  for (const auto& d : stale_deferred_) a.dst0[a.ndst0++] = d.dst;  // (deferred_fit: callers check)
   for (int64_t rank : posted) {
     const HipWorker& w = w_[size_t(rank - 1)];
     a.dst[a.ndst++] = b_.isendbuf + size_t(w.slot) * b_.sl;
@@ -545,6 +672,7 @@ void HipComm::maybe_ahead() {
     if (tail_pending_) fail(MPA_ERROR, "fused tail: the epoch it prepared was not enqueued ahead");
   };
   if (ahead_left_ <= 0 || !b_.await_all || int64_t(call_posts_.size()) != b_.n || !held_.empty()) return skip();
+  run_deferred();  // (launch-ahead runs at nwait = n: a held stale re-dispatch is rare there)
   UpdateSpec& u = ahead_pred_;
   for (const auto& cp : call_posts_)
     if (w_[size_t(cp.rank - 1)].preposted) return skip();
@@ -631,6 +759,9 @@ int64_t HipComm::counter(const char* name) const {
   if (k == "gate_steps") return int64_t(gate_steps_taken());
   if (k == "head_steps") return n_head_;    // epoch steps run at the head of a task launch
   if (k == "epoch_kernels") return n_epoch_;  // epoch steps run as their own epoch kernel
+  if (k == "prearmed") return n_prearmed_;   // head steps whose launch was pre-armed
+  if (k == "stale_deferred") return n_deferred_;  // held re-dispatches whose messages joined the next step
+  if (k == "prearm_cancelled") return n_pre_cancel_;
   return -1;
 }
 

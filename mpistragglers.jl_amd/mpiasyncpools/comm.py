@@ -90,7 +90,8 @@ class _Comm:
 
     def counter(self, name):
         """An event counter of the transport (mpa_comm_counter): "held", "held_joined",
-        "held_alone", "gate_steps", "head_steps", "epoch_kernels"; -1 if the transport does not count it."""
+        "held_alone", "gate_steps", "head_steps", "epoch_kernels", "prearmed", "prearm_cancelled",
+        "stale_deferred"; -1 if the transport does not count it."""
         return int(lib().mpa_comm_counter(self._h, name.encode()))
 
     def set_gate(self, kinds, offsets, ranks):

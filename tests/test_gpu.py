@@ -411,18 +411,24 @@ def test_sampled_timing_counts_one_in_k_launches(M, torch_mod, monkeypatch):
 def test_fused_head_matches_epoch_kernel(M, torch_mod, monkeypatch, dtype, cols):
     """The epoch step at the head of the task launch (flush, every worker posted: c1's loop)
     gives the same iterates, replies and messages bit for bit as the step in its own epoch
-    kernel (MPA_HEAD=0), and it is the one that ran (the transport's counters); nwait < n
-    runs it too, with the pool's bookkeeping intact."""
+    kernel (MPA_HEAD=0), and it is the one that ran (the transport's counters).  With a
+    predicate nwait (not launch-ahead's integer n) the launches are PRE-ARMED (enqueued one
+    epoch early, released through the pinned mailbox): bitwise the same again, with
+    first_plus(n - 1) = every worker fresh, so every epoch is deterministic.  nwait < n runs
+    both, with the pool's bookkeeping intact."""
     import lsq
     torch = torch_mod
     monkeypatch.setenv("MPA_AHEAD", "0")
+    monkeypatch.setenv("MPA_WAIT_TIMEOUT_S", "30")
     n, rows, seed, epochs = 3, 4096, 11, 12
     tdt = torch.float64 if dtype == "f64" else torch.float32
     A = _dev(torch, lsq.gen_matrix(seed, 0, n * rows, cols, dtype))
     b = _dev(torch, lsq.gen_vector(seed, 0, n * rows, dtype))
+    names = ("head_steps", "epoch_kernels", "prearmed", "prearm_cancelled")
 
-    def run(head, nwait):
-        monkeypatch.setenv("MPA_HEAD", "1" if head else "0")
+    def run(nwait, **env):
+        for k in ("MPA_HEAD", "MPA_PREARM"):
+            monkeypatch.setenv(k, env.get(k, "1"))
         comm = M.DeviceComm(n)
         for r in range(1, n + 1):
             comm.set_task_lsq(r, A[(r - 1) * rows:r * rows], b[(r - 1) * rows:r * rows])
@@ -431,25 +437,34 @@ def test_fused_head_matches_epoch_kernel(M, torch_mod, monkeypatch, dtype, cols)
         isend = torch.zeros(n * cols, dtype=tdt, device="cuda")
         recv = torch.zeros(n * cols, dtype=tdt, device="cuda")
         irecv = torch.zeros_like(recv)
-        h0, e0 = comm.counter("head_steps"), comm.counter("epoch_kernels")
+        c0 = [comm.counter(k) for k in names]
         M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, 1e-3, epochs)
         torch.cuda.synchronize()
-        steps = (comm.counter("head_steps") - h0, comm.counter("epoch_kernels") - e0)
+        steps = dict(zip(names, [comm.counter(k) - v for k, v in zip(names, c0)]))
         M.waitall_(pool, recv, irecv)
         torch.cuda.synchronize()
         out = (x.clone(), recv.clone(), isend.clone(), pool.epoch, list(pool.repochs))
         comm.close()
         return out, steps
 
-    on, s_on = run(True, n)
-    off, s_off = run(False, n)
-    assert s_on[0] >= epochs - 1 and s_off[0] == 0 and s_off[1] >= epochs - 1, (s_on, s_off)
-    for a, c in zip(on[:3], off[:3]):
-        assert torch.equal(a, c)
-    assert on[3:] == off[3:]
+    def same(p, q):
+        for a, c in zip(p[:3], q[:3]):
+            assert torch.equal(a, c)
+        assert p[3:] == q[3:]
+
+    on, s_on = run(n)
+    off, s_off = run(n, MPA_HEAD="0")
+    assert s_on["head_steps"] >= epochs - 1 and s_off["head_steps"] == 0 and s_off["epoch_kernels"] >= epochs - 1
+    same(on, off)
     assert float(torch.linalg.norm(on[0])) > 0
-    part, s_part = run(True, n - 1)
-    assert s_part[0] >= 1 and part[3] == epochs and max(part[4]) == epochs
+    allf = M.first_plus(n - 1)
+    pre, s_pre = run(allf)
+    nopre, s_nopre = run(allf, MPA_PREARM="0")
+    assert s_pre["prearmed"] >= epochs - 3 and s_nopre["prearmed"] == 0, (s_pre, s_nopre)
+    same(pre, nopre)
+    same(pre, on)
+    part, s_part = run(n - 1)
+    assert s_part["head_steps"] >= 1 and part[3] == epochs and max(part[4]) == epochs
     assert bool(torch.isfinite(part[0]).all()) and float(torch.linalg.norm(part[0])) > 0
 
 

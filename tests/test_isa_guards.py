@@ -62,3 +62,16 @@ def test_lsqp4_m0_writes_are_separated_and_private(tmp_path):
             m0_in_block = True
         prev = line
     assert m0_writes > 0 and m0_writes <= dma <= 2 * m0_writes
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_lsq_kernels_use_no_scratch(tmp_path):
+    """Every lsq_grad_kernel variant (the fused head and pre-armed ones included) runs without
+    scratch: a pointer that could point at either the kernel-argument EpochArgs or its LDS copy
+    once made the compiler copy the 976-B struct to scratch, 3.5 KiB per workgroup and 50 us per
+    c1 launch (profiles/r03_c1_head_ab.txt)."""
+    text = _asm(tmp_path, "lsq_kernel.hip")
+    sizes = re.findall(r"\.private_segment_fixed_size:\s*(\d+)", text)
+    names = re.findall(r"\.name:\s*(_Z\S*lsq_grad_kernel\S*)", text)
+    assert names and len(sizes) >= len(names), (len(names), len(sizes))
+    assert all(int(s) == 0 for s in sizes), sizes
