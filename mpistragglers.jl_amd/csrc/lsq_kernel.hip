@@ -523,6 +523,22 @@ int c2_variant() {
 
 constexpr int kMode = M_CLAMP | M_DPP | M_NT;  // shipped mode of the other shapes
 
+// rows per wave iteration of the fp64 <= 128-column shape (c1: 4096 x 64 per worker): 16, so
+// a wave's whole share of a c1 task is in flight at once (c1 56-57k against 53-54k it/s with 4,
+// profiles/r03_c1_rb_ab.txt; 4 and 8 stay selectable in the measurement build)
+int small_f64_rb() {
+#if MPA_MEASURE
+  static const int rb = [] {
+    const char* e = std::getenv("MPA_LSQ_SMALL_RB");
+    const int v = e ? std::atoi(e) : 16;
+    return v == 4 || v == 8 ? v : 16;
+  }();
+  return rb;
+#else
+  return 16;
+#endif
+}
+
 }  // namespace
 
 int lsq_cols_pad(int dtype, int cols) {
@@ -549,6 +565,7 @@ int lsq_rows_per_wave_iter(int dtype, int cols) {
     if (cp == 1024) return kC2Variants[c2_variant()].rb;
     return cp < 1024 ? 4 : 2;
   }
+  if (cp == 128) return small_f64_rb();
   return cp <= 256 ? 4 : cp <= 1024 ? 2 : 1;
 }
 
@@ -574,7 +591,12 @@ hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s) {
   }
   if (dtype == MPA_F64) {
     switch (cp) {
-      case 128: return go<double, 1, 4, kMode>(a, s);
+      case 128:
+#if MPA_MEASURE
+        if (small_f64_rb() == 4) return go<double, 1, 4, kMode>(a, s);
+        if (small_f64_rb() == 8) return go<double, 1, 8, kMode>(a, s);
+#endif
+        return go<double, 1, 16, kMode>(a, s);
       case 256: return go<double, 2, 4, kMode>(a, s);
       case 512: return go<double, 4, 2, kMode>(a, s);
       case 1024: return go<double, 8, 2, kMode>(a, s);
