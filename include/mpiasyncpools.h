@@ -196,7 +196,10 @@ int mpa_comm_set_gate(mpa_comm* comm, int64_t nsteps, const int* kinds, const in
  * rank 0: "held" stale re-dispatches whose launch was held (src/MPIAsyncPools.jl:177-184,
  * DESIGN.md §5), "held_joined" of them launched inside a later batch, "held_alone" launched
  * on their own (a wait that would block, a gated release, waitall!, shutdown);
- * "gate_steps" gated-replay steps taken. */
+ * "gate_steps" gated-replay steps taken; "head_steps" / "epoch_kernels" native-loop epoch
+ * steps run at the head of a task launch / as their own kernel, "prearmed" /
+ * "prearm_cancelled" pre-armed launches released / cancelled, "stale_deferred" held
+ * re-dispatches whose copies joined the next epoch step. */
 int64_t mpa_comm_counter(mpa_comm* comm, const char* name);
 /* ---- multi-process communicators: one process per GPU ------- */
 /* placement[w] = the process rank that serves worker w+1 (rank 0 is the coordinator's own
