@@ -38,11 +38,12 @@ METRIC = "iterations/sec + shard-kernel HBM GB/s (% peak), nwait=k of 1/2/4/8 GP
 CONFIGS = {
     # the reference's own CPU example restated on the device: coordinator + 3 workers,
     # nwait = 2 (examples/iterative_example.jl structure; latency-bound)
-    # timing_period: one launch in 16 carries the HIP timing events (their host cost sits on
-    # this config's critical path; every launch of the bandwidth-bound configs carries them)
+    # timing_period: one launch in 16 (c1) / 8 (c2) carries the HIP timing events (their host
+    # cost sits on c1's critical path; c2 +1.3 %, profiles/r03_c1_timing_ab.txt); the few-epoch
+    # configs c3-c5 time every launch
     "c1": dict(rows=3 << 12, cols=64, workers=3, nwait=2, dtype="f64", timing_period=16,
                desc="BASELINE configs[0] shape: 3 workers, fp64 least squares A 3*2^12 x 64, nwait=2 (latency-bound)"),
-    "c2": dict(rows=1 << 20, cols=1024, workers=8, nwait=8, dtype="f32",
+    "c2": dict(rows=1 << 20, cols=1024, workers=8, nwait=8, dtype="f32", timing_period=8,
                desc="BASELINE configs[1]: fp32 least squares A 2^20x1024 row-sharded over 8 logical workers, "
                     "nwait=8 (no stragglers); 1 GPU = 8 stream-workers, N GPUs = 8/N workers per GPU"),
     # the other BASELINE configs at their full global size, 8 workers on ONE GPU (secondary
@@ -309,6 +310,7 @@ def report(args, cfg, world, el, per_rank, extra):
                                              "(this run, timed region only); achieved = alg bytes / busy ms" % (
                                                  "every launch" if tp == 1 else "one in every %d launches" % tp),
                      "timing_sample_period": tp,
+                     "launches_total": extra.pop("launches_total", None),
                      "launches": kl, "busy_ms": round(sum(p[3] for p in per_rank), 3)},
         "epoch_alg_GBps": round(epoch_bytes * its / 1e9, 1),
     }
@@ -454,6 +456,7 @@ def run_single(args, cfg):
     comm.timing()
     comm.set_timing(True, timing_period(args, cfg))
     steps0 = {k: comm.counter(k) for k in ("head_steps", "epoch_kernels", "prearmed", "prearm_cancelled")}
+    launches0 = comm.counter("task_launches")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loop(args.steps)
@@ -463,14 +466,17 @@ def run_single(args, cfg):
     # where the timed region's epoch steps ran: at the head of the task launch, as their own
     # epoch kernel (the rest ride in launch tails, launch-ahead at nwait = n)
     extra["epoch_steps"] = {k: comm.counter(k) - v for k, v in steps0.items()}
+    extra["launches_total"] = comm.counter("task_launches") - launches0  # timed or not
     extra["exchange"] = exchange_report(comm.exchange_timing())
     fresh = int((pool.repochs == pool.epoch).sum())
     # launches after the timed region (waitall releases held stale re-dispatches): counted, so
     # that a kernel trace of this command can drop them from its timed-region window
     # (tools/trace_window.py)
+    l_end = comm.counter("task_launches")
     M.waitall_(pool, recv, irecv)
     torch.cuda.synchronize()
-    extra["launches_after_timed"] = comm.timing()[0]
+    extra["launches_after_timed"] = comm.counter("task_launches") - l_end
+    comm.timing()
     comm.set_timing(False)
     extra["measured_read_peak"] = read_peak(M, torch)
     extra.update({"x_norm": float(torch.linalg.norm(x.float()).item()), "build": M.lib().mpa_build_info().decode(),

@@ -678,6 +678,7 @@ HipComm::LsqbLaunch HipComm::build_lsqb_batch(const std::vector<int64_t>& ranks,
 }
 
 void HipComm::enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int64_t armed_rank) {
+  n_task_launches_.fetch_add(1, std::memory_order_relaxed);
   TimedLaunch tl{};
   const bool timed = sample_task(armed_rank);
   if (timed) {
@@ -704,6 +705,7 @@ void HipComm::enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int
 
 void HipComm::enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s, double bytes, int64_t armed_rank,
                           bool untimed) {
+  n_task_launches_.fetch_add(1, std::memory_order_relaxed);
   TimedLaunch tl{};
   // a pre-armed launch is never timed (it waits for the host inside); the launch pre-arming
   // skipped for the timing's sake always is

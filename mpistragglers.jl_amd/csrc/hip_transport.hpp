@@ -778,6 +778,7 @@ class HipComm final : public Comm {
   std::atomic<bool> timing_{false};  // read by the straggler timer thread's launches
   int timing_period_ = 1;
   std::atomic<uint64_t> t_seq_{0};  // task launches seen while timing (the timer thread launches too)
+  std::atomic<int64_t> n_task_launches_{0};  // every task launch ("task_launches")
   uint64_t x_seq_ = 0;              // epoch kernels seen while timing
   bool sample_task(int64_t armed_rank) {
     if (!timing_) return false;

@@ -760,7 +760,8 @@ int64_t HipComm::counter(const char* name) const {
   if (k == "head_steps") return n_head_;    // epoch steps run at the head of a task launch
   if (k == "epoch_kernels") return n_epoch_;  // epoch steps run as their own epoch kernel
   if (k == "prearmed") return n_prearmed_;   // head steps whose launch was pre-armed
-  if (k == "stale_deferred") return n_deferred_;  // held re-dispatches whose messages joined the next step
+  if (k == "stale_deferred") return n_deferred_;
+  if (k == "task_launches") return n_task_launches_.load(std::memory_order_relaxed);  // least-squares launches  // held re-dispatches whose messages joined the next step
   if (k == "prearm_cancelled") return n_pre_cancel_;
   return -1;
 }

@@ -41,7 +41,9 @@ def test_contract_keys_and_throughput():
     assert r["measured_read_peak"] == 7200.0
     assert abs(r["frac_of_measured_read_peak"] - r["achieved"] / 7200.0) < 1e-3
     assert r["traffic"] is None or r["traffic"] > alg  # PMC file (profiles/) when present
-    assert r["timing_sample_period"] == 1 and "every launch" in r["avg_launch_ms_source"]
+    assert r["timing_sample_period"] == 8 and "one in every 8 launches" in r["avg_launch_ms_source"]
+    out5 = bench.report(_args(), _cfg("c5"), 1, 0.1, [(100, 60.0, 100 * alg, 60.0)], {})
+    assert out5["roofline"]["timing_sample_period"] == 1 and "every launch" in out5["roofline"]["avg_launch_ms_source"]
 
 
 def test_c1_samples_its_timing_events():
@@ -53,7 +55,7 @@ def test_c1_samples_its_timing_events():
     assert r["timing_sample_period"] == 16 and "one in every 16 launches" in r["avg_launch_ms_source"]
     a = _args()
     a.timing_period = 1
-    assert bench.timing_period(a, cfg) == 1 and bench.timing_period(_args(), _cfg("c2")) == 1
+    assert bench.timing_period(a, cfg) == 1 and bench.timing_period(_args(), _cfg("c2")) == 8
 
 
 def test_multi_gpu_rate_is_per_gpu_average_and_no_traffic():

@@ -26,7 +26,8 @@ def main():
     a = p.parse_args()
     line = [ln for ln in open(a.bench_log) if ln.startswith("{")][-1]
     bench = json.loads(line)
-    n = int(bench["roofline"]["launches"])
+    # every launch of the timed region (launches_total), not only the ones the bench timed
+    n = int(bench["roofline"].get("launches_total") or bench["roofline"]["launches"])
     rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     tail = a.tail if a.tail is not None else int(bench.get("launches_after_timed", 0))
