@@ -28,7 +28,7 @@ extern int g_lsq_grid;
 Comm* make_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg);
 void hip_serve(Comm* c);
 void hip_pause_servers(Comm* c);
-void hip_set_defer_end(Comm* c, bool on);
+void hip_set_defer_end(Comm* c, bool on, bool prearm_ok = false);
 void hip_stage_update(Comm* c, int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x, void* mirror,
                       bool msg_bf16);
 void hip_set_ahead(Comm* c, int64_t left, int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x,
@@ -466,7 +466,11 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
       if (on) mpa::hip_set_defer_end(c, false);
     }
   } restore{c, fuse};
-  if (fuse) mpa::hip_set_defer_end(c, true);
+  // pre-armed launches wait on the GPU for the host's next decision: only where nothing but
+  // native code runs between two calls (an integer nwait or the native first_plus predicate; a
+  // caller's predicate could touch the GPU and wait behind the armed launch)
+  const bool prearm_ok = nwait_kind == MPA_NWAIT_INT || (nwait_kind == MPA_NWAIT_FN && nwait_fn == &mpa_nwait_first_plus);
+  if (fuse) mpa::hip_set_defer_end(c, true, prearm_ok);
   for (int64_t e = 0; e < epochs; ++e) {
     if (ahead) {
       rc = guarded([&] {

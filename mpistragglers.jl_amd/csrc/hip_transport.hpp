@@ -272,9 +272,10 @@ class HipComm final : public Comm {
     return w.remote && w.path_known ? (w.path_dev ? int(kPathDevice) : int(kPathHost)) : 0;
   }
   // end_call() leaves the call's harvests pending (they join the next flush's epoch kernel)
-  void set_defer_end_flush(bool on) {
+  void set_defer_end_flush(bool on, bool prearm_ok = false) {
     if (!on) cancel_pre();
     defer_end_ = on;
+    prearm_loop_ = on && prearm_ok;
     if (!on) tail_next_ = tail_pending_ = head_next_ = false;  // the descent loop ended (or failed)
   }
   void stage_update(const UpdateSpec& u);
@@ -710,6 +711,7 @@ class HipComm final : public Comm {
     EpochArgs ep;
   };
   bool prearm_ = true;
+  bool prearm_loop_ = false;  // the running descent loop allows it (set_defer_end_flush)
   bool pre_active_ = false;
   bool pre_vec_ = false;
   PreMailbox* pre_mb_ = nullptr;  // host-pinned, coherent

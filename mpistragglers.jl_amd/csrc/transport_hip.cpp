@@ -347,7 +347,8 @@ void HipComm::flush() {
 // nwait < n (launch-ahead and the fused tail cover nwait = n), right after a fused-head launch
 // of the whole pool, and not for the one launch in `timing_period_` that the timing samples.
 void HipComm::maybe_prearm(int dtype) {
-  if (!prearm_ || !defer_end_ || b_.await_all || gated() || role_ != SOLO || pre_active_ || !held_.empty()) return;
+  if (!prearm_ || !prearm_loop_ || !defer_end_ || b_.await_all || gated() || role_ != SOLO || pre_active_ || !held_.empty())
+    return;
   if (timing_ && timing_period_ > 1 && ++pre_count_ % timing_period_ == 0) {
     time_next_ = true;
     return;
@@ -853,7 +854,7 @@ HipComm::UpdateSpec update_spec(int dtype, int64_t elems, const double* w, int64
 }
 }  // namespace
 
-void hip_set_defer_end(Comm* c, bool on) { static_cast<HipComm*>(c)->set_defer_end_flush(on); }
+void hip_set_defer_end(Comm* c, bool on, bool prearm_ok) { static_cast<HipComm*>(c)->set_defer_end_flush(on, prearm_ok); }
 void hip_stage_update(Comm* c, int dtype, int64_t elems, const double* w, int64_t n, double eta, void* x, void* mirror,
                       bool msg_bf16) {
   static_cast<HipComm*>(c)->stage_update(update_spec(dtype, elems, w, n, eta, x, mirror, msg_bf16));
