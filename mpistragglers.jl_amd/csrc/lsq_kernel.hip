@@ -121,6 +121,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   using P = Pack<T>;
   constexpr int E = P::E;
   __shared__ P red[VPL * 64];           // workgroup partial (VPL*64*E columns)
+  __shared__ P red2[VPL == 1 ? 3 * 64 : 1];  // the one-level tree's partial sums 1-3
   __shared__ unsigned s_ticket, s_cancel;
 
   // which task of the batch this workgroup serves (wave-uniform scan over <= 16 entries)
@@ -338,7 +339,48 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       if (c0 + e < a.cols) out[c0 + e] = s.v[e];
   };
   bool cx = false;  // cancelled (read by the reply's writer only)
-  if (G == 1) {
+  // One-level tree for small partials (one 16-B vector per lane, <= 64 workgroups: c1's tasks):
+  // every workgroup stores its partial and counts in; the last one sums all G of them, four
+  // threads per vector each over every fourth partial in order, then the four sums in order
+  // in LDS -- one counter round trip and one load round instead of two of each.
+  constexpr bool kOneLevel = (S == 64) && (MODE & M_PREFETCH) == 0 && (MODE & M_TREE_FENCE) == 0;
+  if (kOneLevel && G > 1 && G <= 64) {
+    for (int j = tid; j < S; j += kThreads) st_sc1(&slab[size_t(blk) * S + j], red[j]);
+    drain_vm();
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(&a.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_ticket = old + 1 == G;
+      if (s_ticket) __hip_atomic_store(&a.ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_ticket) return;
+    cx = cancelled();
+    const int j = tid & (S - 1), q = tid / S;  // kThreads = 4 * S: four partial sums per vector
+    P acc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc.v[e] = T(0);
+    P t[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+      if (q + 4 * m < int(G)) t[m] = ld_sc1(&slab[size_t(q + 4 * m) * S + j]);
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+      if (q + 4 * m < int(G))
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc.v[e] = m == 0 ? t[m].v[e] : acc.v[e] + t[m].v[e];
+    __syncthreads();  // red[] is free again: the four sums of every vector
+    if (q > 0) red2[(q - 1) * S + j] = acc;
+    __syncthreads();
+    if (q == 0 && !cx) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+        if (r + 1 < int(G))
+#pragma unroll
+          for (int e = 0; e < E; ++e) acc.v[e] += red2[r * S + j].v[e];
+      store_out(j, acc);
+    }
+  } else if (G == 1) {
     cx = cancelled();
     if (!cx)
       for (int j = tid; j < S; j += kThreads) store_out(j, red[j]);
