@@ -455,7 +455,7 @@ def run_single(args, cfg):
     progress("warmup done (%d epochs)" % args.warmup)
     comm.timing()
     comm.set_timing(True, timing_period(args, cfg))
-    steps0 = {k: comm.counter(k) for k in ("head_steps", "epoch_kernels", "prearmed", "prearm_cancelled")}
+    steps0 = {k: comm.counter(k) for k in ("head_steps", "epoch_kernels", "prearmed", "prearm_cancelled", "prearm_same")}
     launches0 = comm.counter("task_launches")
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -722,6 +722,9 @@ class HipComm final : public Comm {
   std::vector<uint8_t*> pre_out_;
   int64_t n_prearmed_ = 0, n_pre_cancel_ = 0, pre_count_ = 0;
   bool time_next_ = false;  // the next normal launch is timed (pre-arming skipped for it)
+  EpochArgs pre_pred_{};    // the step the pre-armed launch carries as its prediction
+  bool pre_same_ = true;    // MPA_PRESAME=0: always release through the mailbox
+  int64_t n_pre_same_ = 0;
   bool pre_consume();
   void maybe_prearm(int dtype);
   // Held stale re-dispatches in the descent loop (flush_stale): their message copies (and the

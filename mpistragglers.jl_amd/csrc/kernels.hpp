@@ -134,6 +134,7 @@ constexpr int kMaxLsqTasks = 16;
 constexpr int kHeadPrearmed = 4;
 constexpr uint32_t kHeadCancel = 0x80000000u;
 constexpr unsigned long long kPreCancel = 1ull << 63;
+constexpr unsigned long long kPreSame = 1ull << 62;  // the step's arguments are `ep` as launched
 struct LsqBatch {
   int ntasks;
   unsigned* err;
@@ -164,7 +165,9 @@ struct LsqBatch {
   //   head | kHeadPrearmed: a PRE-ARMED launch, enqueued one epoch early (transport_hip.cpp,
   //   maybe_prearm): workgroup 0 first waits for the host to decide the epoch -- *pre_go (a
   //   host-pinned word) reaching pre_token -- and reads the step's EpochArgs from *pre_ep (the
-  //   same pinned mailbox) instead of `ep`; pre_token | kPreCancel cancels the launch (every
+  //   same pinned mailbox) instead of `ep` -- or, go = pre_token | kPreSame, the `ep` it was
+  //   launched with (the host's prediction held: no mailbox read over the bus); pre_token |
+  //   kPreCancel cancels the launch (every
   //   workgroup returns, nothing is published).  Bounded like the other waits (err bit 128).
   int head;
   uint32_t* head_word;

@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
           int go = 1;
           unsigned long long v;
           for (unsigned k = 0; ((v = __hip_atomic_load(batch.pre_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) &
-                                ~kPreCancel) != batch.pre_token;
+                                ~(kPreCancel | kPreSame)) != batch.pre_token;
                ++k) {
             if ((k & 255) == 255 && rt_now() - t0s > batch.spin_ticks) {
               __hip_atomic_fetch_or(batch.err, 128u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -209,6 +209,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
             }
           }
           if (v & kPreCancel) go = 0;
+          else if (v & kPreSame) go = 2;
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the mailbox the host wrote
           s_go = go;
         }
@@ -218,10 +219,12 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
             __hip_atomic_store(batch.head_word, batch.head_token | kHeadCancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return;
         }
+        // the arguments into LDS: from the mailbox over the bus, or (s_go == 2: the host's
+        // prediction held) from the kernel arguments it was launched with
         constexpr int kEpVecs = int(sizeof(EpochArgs) / 16);
         static_assert(sizeof(EpochArgs) % 16 == 0, "EpochArgs copies in 16-B vectors");
-        for (int k = tid; k < kEpVecs; k += kThreads)
-          reinterpret_cast<uint4*>(&s_ep)[k] = reinterpret_cast<const uint4*>(batch.pre_ep)[k];
+        const uint4* src = s_go == 2 ? reinterpret_cast<const uint4*>(&batch.ep) : reinterpret_cast<const uint4*>(batch.pre_ep);
+        for (int k = tid; k < kEpVecs; k += kThreads) reinterpret_cast<uint4*>(&s_ep)[k] = src[k];
         __syncthreads();
         if ((batch.head & 3) == 2) epoch_elems<T, E, true>(s_ep, tid, kThreads);
         else epoch_elems<T, 1, true>(s_ep, tid, kThreads);
