@@ -240,7 +240,15 @@ def exchange_report(xt):
 
 
 def timing_period(args, cfg):
-    return args.timing_period if getattr(args, "timing_period", None) else cfg.get("timing_period", 1)
+    """HIP events on one launch in k: the config's k, lowered so that a short run still times
+    at least 16 launches (a 20-step c2 line at 1 in 8 timed only 3)."""
+    if getattr(args, "timing_period", None):
+        return args.timing_period
+    k = cfg.get("timing_period", 1)
+    steps = getattr(args, "steps", None)
+    if steps:
+        k = max(1, min(k, steps // 16))
+    return k
 
 
 def report(args, cfg, world, el, per_rank, extra):

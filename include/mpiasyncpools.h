@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define MPA_ABI_VERSION 3
+#define MPA_ABI_VERSION 4
 
 typedef struct mpa_pool mpa_pool;
 typedef struct mpa_comm mpa_comm;
@@ -192,14 +192,26 @@ int mpa_comm_shutdown(mpa_comm* comm);
  * oracle's trace bit for bit whatever the physical completion order. */
 int mpa_comm_set_gate(mpa_comm* comm, int64_t nsteps, const int* kinds, const int64_t* offsets,
                       const int64_t* ranks);
+/* gated replay, paced (HIP rank 0): the virtual completion times of worker `rank`'s tasks
+ * 1..count on the oracle's clock (ns from the first call of the replay, OracleSim.events).
+ * While the gate is on, a delayed task of that worker is launched so that it completes at
+ * the replay's start + done_ns[task - 1] instead of `delay` after its dispatch: the host time
+ * the harness spends between calls (which the oracle's coordinator does not) then cannot
+ * accumulate along a worker's chain of tasks into its latencies.  count == 0 clears it. */
+int mpa_comm_set_gate_clock(mpa_comm* comm, int64_t rank, const int64_t* done_ns, int64_t count);
 /* event counters (tests, diagnostics); -1 for a name the transport does not count.  HIP
  * rank 0: "held" stale re-dispatches whose launch was held (src/MPIAsyncPools.jl:177-184,
  * DESIGN.md §5), "held_joined" of them launched inside a later batch, "held_alone" launched
  * on their own (a wait that would block, a gated release, waitall!, shutdown);
  * "gate_steps" gated-replay steps taken; "head_steps" / "epoch_kernels" native-loop epoch
  * steps run at the head of a task launch / as their own kernel, "prearmed" /
- * "prearm_cancelled" pre-armed launches released / cancelled, "stale_deferred" held
- * re-dispatches whose copies joined the next epoch step. */
+ * "prearm_cancelled" pre-armed launches released / cancelled, "prearm_same" pre-armed
+ * launches released with the step they predicted (no mailbox read), "stale_deferred" held
+ * re-dispatches whose copies joined the next epoch step, "task_launches"
+ * least-squares task launches, "armed" (worker process) tasks launched device-armed,
+ * "sleeps" delayed tasks that slept on the device (MPA_DELAY=device), "timer_late" delayed
+ * launches the host timer issued more than 1 ms after they were due, "queues" CU-masked streams (HSA queues) the process holds on the comm's device,
+ * "shared_worker_streams" workers whose stream is shared past the queue cap. */
 int64_t mpa_comm_counter(mpa_comm* comm, const char* name);
 /* ---- multi-process communicators: one process per GPU ------- */
 /* placement[w] = the process rank that serves worker w+1 (rank 0 is the coordinator's own

@@ -1,41 +1,73 @@
 // HipComm, task launches: registration-time scratch (prepare_*), batching the tasks of a
 // flush into one launch per kernel, kernel arguments of the least-squares kernels (c1-c5),
-// the straggler timer thread (injected delays), HIP-event timing, and the process-wide pool
-// of CU-masked streams.
+// injected straggler delays (host timer thread, or a sleep kernel on the worker's stream),
+// HIP-event timing, and
+// the process-wide, capped set of CU-masked streams.
 #include "hip_transport.hpp"
 
 namespace mpa {
 
 int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares launch (0 = default)
 
-// Process-wide pool of CU-masked streams: communicators come and go (tests create many),
-// but the HSA queues behind their streams are a bounded hardware resource, so a destroyed
-// comm returns its streams here and the next comm reuses them instead of growing the
-// process's queue count (more queues than the hardware maps at once are time-sliced).
+// Process-wide set of CU-masked streams (each its own HSA queue).  Communicators come and go
+// (tests create many), but the queues are a bounded hardware resource: once a device carries
+// more queues than the scheduler maps at once, it time-slices them, and a launch on an
+// unmapped queue waits up to ~10 ms for its turn -- also inside the launch call.  Measured
+// (profiles/r04_queue_latency.txt, tools/probe_queue_latency.hip): launch -> visible of a
+// one-wave kernel on a random idle queue, max 27 us with up to 20 CU-masked queues in the
+// process, p99 8.4 ms with 24, 34 of 150 launches > 1 ms with 32; the gated kmap2_n9 replay
+// ran within 1.5 ms of the oracle until a 24-worker comm grew the pool, then 578-643
+// harvests were 1-25 ms late (r04_gated_stall.txt).  So the process holds at most
+// queue_cap() of them per device (MPA_MAX_QUEUES, default 12, leaving room for the runtime's
+// and torch's own); a comm returns its streams here, the next one reuses them, and past the
+// cap workers share the least-used stream (a delayed worker then sleeps on a shared queue:
+// stream_shared()).
+struct QueueStream {
+  int device;
+  hipStream_t s;
+  int users;
+};
 std::mutex g_stream_mu;
-std::vector<std::pair<int, hipStream_t>> g_free_streams;
+std::vector<QueueStream> g_streams;
 
-// The pooled streams (and their HSA queues) are destroyed at process exit, before the HIP
+static int queue_cap() {
+  static const int cap = [] {
+    const char* e = std::getenv("MPA_MAX_QUEUES");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : kDefaultMaxQueues;
+  }();
+  return cap;
+}
+
+// The streams (and their HSA queues) are destroyed at process exit, before the HIP
 // runtime's own teardown (atexit handlers run in reverse registration order, and the runtime
 // registers its teardown when it is loaded, before the first stream here): a profiler that
 // tears down while queues are still alive crashed in __cxa_finalize.
 void destroy_pooled_streams() {
   std::lock_guard<std::mutex> lk(g_stream_mu);
-  for (auto& ds : g_free_streams) (void)hipStreamDestroy(ds.second);
-  g_free_streams.clear();
+  for (auto& q : g_streams) (void)hipStreamDestroy(q.s);
+  g_streams.clear();
 }
 
 hipStream_t make_queue_stream(int device) {
   static const bool registered = (std::atexit(destroy_pooled_streams), true);
   (void)registered;
-  {
-    std::lock_guard<std::mutex> lk(g_stream_mu);
-    for (size_t k = 0; k < g_free_streams.size(); ++k)
-      if (g_free_streams[k].first == device) {
-        hipStream_t s = g_free_streams[k].second;
-        g_free_streams.erase(g_free_streams.begin() + std::ptrdiff_t(k));
-        return s;
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  int have = 0;
+  for (auto& q : g_streams)
+    if (q.device == device) {
+      if (q.users == 0) {
+        q.users = 1;
+        return q.s;
       }
+      ++have;
+    }
+  if (have >= queue_cap()) {  // share the least-used one
+    QueueStream* best = nullptr;
+    for (auto& q : g_streams)
+      if (q.device == device && (!best || q.users < best->users)) best = &q;
+    best->users += 1;
+    return best->s;
   }
   hipDeviceProp_t p;
   HIPCHECK(hipGetDeviceProperties(&p, device));
@@ -44,13 +76,32 @@ hipStream_t make_queue_stream(int device) {
   if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
   hipStream_t s = nullptr;
   HIPCHECK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+  g_streams.push_back({device, s, 1});
   return s;
 }
 
 void release_queue_stream(int device, hipStream_t s) {
   (void)hipStreamSynchronize(s);
   std::lock_guard<std::mutex> lk(g_stream_mu);
-  g_free_streams.push_back({device, s});
+  for (auto& q : g_streams)
+    if (q.device == device && q.s == s && q.users > 0) {
+      q.users -= 1;
+      return;
+    }
+}
+
+bool stream_shared(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  for (const auto& q : g_streams)
+    if (q.s == s) return q.users > 1;
+  return false;
+}
+
+int queue_streams(int device) {
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  int k = 0;
+  for (const auto& q : g_streams) k += q.device == device;
+  return k;
 }
 
 void HipComm::prepare_lsq(int64_t rank, const TaskSpec& ts) {
@@ -214,20 +265,21 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
       continue;
     }
     // The message is delivered now (stream-ordered after the exchange / stage-in); a
-    // delayed worker "sleeps" on the host timer and only then computes.
-    if (staged) stage_in({rank}, worker_stream(w));
-    else after_exchange(worker_stream(w));
+    // delayed worker "sleeps" and only then computes: on the host timer thread, which
+    // launches the task when it is due (default), or on the device, a sleep kernel queued
+    // ahead of the task on the worker's stream (MPA_DELAY=device).
+    hipStream_t s = worker_stream(w);
+    if (staged) stage_in({rank}, s);
+    else after_exchange(s);
     std::function<void()> go;
     if (ts.kind == MPA_TASK_LSQ) {
       double bytes = 0;
       const LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes);
       const int cols = int(ts.cols), dt = ts.dtype;
-      hipStream_t s = w.stream;
       go = [this, b, dt, cols, s, bytes]() { enqueue_lsq(b, dt, cols, s, bytes); };
     } else if (ts.kind == MPA_TASK_LSQ_BATCH) {
       double bytes = 0;
       const LsqbLaunch b = build_lsqb_batch({rank}, &bytes);
-      hipStream_t s = w.stream;
       go = [this, b, s, bytes]() { enqueue_lsqb(b, s, bytes); };
     } else {
       KmapArgs a{};
@@ -238,11 +290,25 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
       a.out = w.out;
       a.rl = w.rl;
       a.pub = Publish{w.flag_dev, err_dev_, w.seq, spin_ticks()};
-      hipStream_t s = w.stream;
       go = [a, s]() { HIPCHECK(launch_kmap(a, s)); };
     }
-    if (delay > 0) defer(mono_ns() + uint64_t(delay), std::move(go));
-    else go();
+    // The oracle's worker replies exactly `delay` after its post; a launched task takes
+    // ~30-40 us more (launch, the kernel, the completion word crossing the bus).  That
+    // overhead is taken out of the sleep (delay_lead_ns_), or it would accumulate along every
+    // worker's chain of tasks: the gated kmap2_n9 replay drifted 1.2-1.9 ms from the
+    // oracle's latencies by its 100th call with 40 us per task (profiles/r04_gated_stall.txt).
+    int64_t sleep_ns = delay - delay_lead_ns_;
+    // a paced gated replay: complete when the oracle's clock says (mpa_comm_set_gate_clock)
+    if (const uint64_t due = delay > 0 ? gate_due(rank, w.seq) : 0) sleep_ns = int64_t(due) - int64_t(mono_ns()) - delay_lead_ns_;
+    if (sleep_ns > 0 && delay_on_device_) {
+      HIPCHECK(launch_sleep((unsigned long long)(double(sleep_ns) * rt_hz_ / 1e9), s));
+      n_sleeps_ += 1;
+      go();
+    } else if (sleep_ns > 0) {
+      defer(mono_ns() + uint64_t(sleep_ns), std::move(go));
+    } else {
+      go();
+    }
   }
   emit();
 }
@@ -269,8 +335,10 @@ void HipComm::timer_loop() {
       continue;
     }
     const uint64_t due = deferred_.front().due, now = mono_ns();
-    if (now + 200000 < due) {  // sleep to ~100 us before the deadline, then spin
-      tcv_.wait_for(lk, std::chrono::nanoseconds(due - now - 100000));
+    // sleep to ~1 ms before the deadline, then spin: a condition-variable wake-up came up to
+    // 0.6 ms late on a busy box (profiles/r04_gated_stall.txt, round 3's 100 us lead)
+    if (now + kTimerSpinNs + 100000 < due) {
+      tcv_.wait_for(lk, std::chrono::nanoseconds(due - now - kTimerSpinNs));
       continue;
     }
     if (now < due) {
@@ -284,6 +352,8 @@ void HipComm::timer_loop() {
     deferred_.pop_back();
     tbusy_ = true;
     lk.unlock();
+    const uint64_t t_go = mono_ns();
+    if (t_go - d.due > 1000000) n_timer_late_.fetch_add(1, std::memory_order_relaxed);
     try {
       d.go();
     } catch (const Failure&) {

@@ -97,7 +97,11 @@ void HipComm::serve() {
 // Device-armed tasks: least-squares workers without injected delays whose
 // messages arrive in this GPU's slot (device payload path).  MPA_ARM: 0 never, 1 every such
 // worker, 2 (default) where the process serves one worker (the N = 8 placement; a process
-// with several workers launches the tasks of a flush as one batch instead).
+// with several workers launches the tasks of a flush as one batch instead).  The in-kernel
+// wait (MPA_ARM_WAIT=kernel: every workgroup of the armed launch waits) is refused by the
+// default on a GPU that rank 0 also uses: the waiting grids held the CUs rank 0's kernels
+// needed to ring them (profiles/r03_rehearsal_n248.txt); the default one-wave
+// wait (door_wait_kernel) holds nothing anyone needs.
 bool HipComm::armable(int64_t rank) const {
   const TaskSpec& ts = tasks_[size_t(rank - 1)];
   const HipWorker& w = w_[size_t(rank - 1)];
@@ -105,14 +109,17 @@ bool HipComm::armable(int64_t rank) const {
     return false;
   if (arm_mode_ == 1) return true;
   int here = 0;
-  for (const auto& w : w_) here += w.here;
-  return here == 1;
+  for (const auto& v : w_) here += v.here;
+  if (here != 1) return false;
+  return arm_wave_ || w.box->coord_dev != dev_;
 }
 
-// The worker's next task is launched before rank 0 posts it: every workgroup waits in-kernel
-// for the worker's device doorbell (wait_door), which rank 0's exchange / epoch kernel stores
-// over xGMI right after the message, so ring -> start is a poll of this GPU's memory instead
-// of the serve loop's host poll and a launch (19 us of the traced c2 N = 2 epoch).
+// The worker's next task is launched before rank 0 posts it and waits for the worker's device
+// doorbell, which rank 0's exchange / epoch kernel stores over xGMI right after the message, so
+// ring -> start is a poll of this GPU's memory instead of the serve loop's host poll and a
+// launch (19 us of the traced c2 N = 2 epoch).  Default: a one-wave door_wait_kernel with the
+// task queued behind it; MPA_ARM_WAIT=kernel: the task kernel's own in-kernel wait (wait_door,
+// every workgroup).  Either way the task reads its go word (a cancel) before it replies.
 void HipComm::arm(int64_t rank) {
   HipWorker& w = w_[size_t(rank - 1)];
   const TaskSpec& ts = tasks_[size_t(rank - 1)];
@@ -126,19 +133,23 @@ void HipComm::arm(int64_t rank) {
   w.rl = w.sl * (ts.kind == MPA_TASK_LSQ_BATCH ? 2 : 1);
   w.x = w.xslot;
   w.out = reply_dst(w);
+  hipStream_t st = worker_stream(w);
+  unsigned long long* door = arm_wave_ ? nullptr : own_door(w);
+  if (arm_wave_) HIPCHECK(launch_door_wait(own_door(w), s, spin_ticks(), err_dev_, st));
   double bytes = 0;
   if (ts.kind == MPA_TASK_LSQ) {
     LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes, armed_share());
     b.t[0].go = w.cancel_dev;
-    b.t[0].door = own_door(w);
-    enqueue_lsq(b, ts.dtype, int(ts.cols), worker_stream(w), bytes, rank);
+    b.t[0].door = door;
+    enqueue_lsq(b, ts.dtype, int(ts.cols), st, bytes, rank);
   } else {
     LsqbLaunch b = build_lsqb_batch({rank}, &bytes, armed_share());
     b.set_go(w.cancel_dev);
-    b.set_door(own_door(w));
-    enqueue_lsqb(b, worker_stream(w), bytes, rank);
+    b.set_door(door);
+    enqueue_lsqb(b, st, bytes, rank);
   }
   w.armed = true;
+  n_armed_ += 1;
 }
 
 void HipComm::disarm_all() {

@@ -13,8 +13,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
 #include <cstdio>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -56,6 +56,10 @@ constexpr int kDefaultLaunchGrid = 192;
 constexpr int kWideResidGrid = 1024;  // wide rows: pass-1 workgroups per launch (a wave per row)
 constexpr int kSlabGridCap = kLsqMaxGrid;  // most workgroups a single task may be given
 constexpr int kLaunchStreams = 2;
+constexpr uint64_t kTimerSpinNs = 1000000;
+// A delayed task's own overhead (launch -> completion word seen, ~30-40 us: the median latency
+// deviation of the gated replays, profiles/r04_gated_stall.txt) comes out of its sleep.
+constexpr int64_t kDelayLeadNs = 35000;  // the straggler timer spins the last 1 ms before a due launch
 // batched multi-iterate task: pass-1 / pass-2 workgroups per launch (= resident: 1 x 512 /
 // 2 x 256 threads per CU by VGPRs), and the most row ranges a pass-2 task is split into
 constexpr int kLsqbGrid1 = 512;  // two 8-wave workgroups per CU: pass 1 4.74-4.88 -> 5.11 TB/s (profiles/r01_lsqb_grid.txt)
@@ -76,11 +80,16 @@ inline int lsqb_grid(int pass) {
   return pass == 1 ? g1 : g2;
 }
 
-// Process-wide pool of CU-masked streams (hip_launch.cpp): communicators come and go
+// Process-wide, capped set of CU-masked streams (hip_launch.cpp): communicators come and go
 // (tests create many), but the HSA queues behind their streams are a bounded hardware
-// resource, so a destroyed comm returns its streams to the pool and the next comm reuses them.
+// resource (past ~20 per device the scheduler time-slices them and launches stall up to
+// ~10 ms), so a destroyed comm returns its streams and the next comm reuses them; past the
+// cap (MPA_MAX_QUEUES) streams are shared.
+constexpr int kDefaultMaxQueues = 12;
 hipStream_t make_queue_stream(int device);
 void release_queue_stream(int device, hipStream_t s);
+bool stream_shared(hipStream_t s);  // more than one worker / comm launches on it
+int queue_streams(int device);      // CU-masked streams the process holds on the device
 
 struct HipWorker {
   bool here = true;     // its tasks run in this process
@@ -332,7 +341,7 @@ class HipComm final : public Comm {
                                          : size_t(ts.cols) * (ts.dtype == MPA_F64 ? 8 : 4);
   }
 
-  // launch task seq+1 of `rank` on its stream, waiting in-kernel for the device doorbell
+  // launch task seq+1 of `rank` on its stream, behind a wait for the device doorbell
   void arm(int64_t rank);
 
   // release every waiting armed task: one whose doorbell rank 0 has not rung is cancelled
@@ -471,10 +480,13 @@ class HipComm final : public Comm {
   // ---- straggler emulation -------------------------------------------------------------
   // A worker with a delay schedule sleeps `delay` ns after its message is delivered and
   // then computes (the reference worker's `sleep(rand())` before its reply,
-  // examples/iterative_example.jl:74).  The sleep is a host timer thread that launches the
-  // task kernel when it is due, so a sleeping worker holds no GPU queue: kernels parked
-  // in queues (a spinning delay kernel) made one straggler hold back another once the
-  // process had more streams than the GPU maps hardware queues for.
+  // examples/iterative_example.jl:74).  Default: a host timer thread launches the task kernel
+  // when it is due, so a sleeping worker has nothing queued on the GPU.  MPA_DELAY=device: a
+  // one-wave sleep kernel queued ahead of the task on the worker's stream instead -- exact on
+  // the device clock, but CU-masked streams are blocking streams, so every operation a
+  // caller issues on the legacy NULL stream then waits for every sleeping straggler
+  // (profiles/r04_delay_on_device.txt).  Round 3's ~20 ms outliers were the process's queue
+  // count, not the timer (profiles/r04_gated_stall.txt).
   static uint64_t mono_ns() {
     return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count());
   }
@@ -791,6 +803,7 @@ class HipComm final : public Comm {
   }
   bool debug_ = false;
   int arm_mode_ = 0;
+  bool arm_wave_ = true;  // MPA_ARM_WAIT: an armed task waits behind a one-wave door_wait_kernel
   bool batch_gather_ = true;  // MPA_GATHER=0: a server launches whatever one doorbell scan found
   // undelayed task batches run on the coordinator stream behind the exchange that delivered
   // their messages (MPA_COORD_BATCH=0: on a launch stream behind a cross-queue event wait,
@@ -814,6 +827,11 @@ class HipComm final : public Comm {
   std::atomic<bool> tfailed_{false};
   std::mutex tfail_mu_;
   std::string tfail_msg_;
+  std::atomic<int64_t> n_timer_late_{0};  // deferred launches issued > 1 ms after due (counter 'timer_late')
+  bool delay_on_device_ = false;          // MPA_DELAY=device: sleep kernels instead of the timer
+  int64_t delay_lead_ns_ = kDelayLeadNs;  // MPA_DELAY_LEAD_NS: a delayed task's launch overhead, out of its sleep
+  int64_t n_sleeps_ = 0;
+  int64_t n_armed_ = 0;   // server: tasks launched device-armed (counter 'armed')  // delayed tasks (a sleep kernel before the task, counter 'sleeps')
 
  public:
   void init_ticket() {

@@ -252,6 +252,52 @@ hipError_t launch_door_cas(unsigned long long* door, unsigned long long expect, 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// A device-armed task's doorbell wait as a kernel of its own (hip_server.cpp arm, the
+// default MPA_ARM_WAIT=wave): ONE wave polls the worker's device doorbell (wait_door's loop:
+// relaxed system-scope loads, s_sleep, bounded, then one system-scope acquire) and exits;
+// the task kernel queued behind it on the worker's stream starts when the packet processor
+// moves on.  A waiting armed task holds one wave instead of its whole launch grid, so armed
+// worker processes sharing a GPU with rank 0 (a one-GPU rehearsal) cannot starve the
+// kernels that ring their doorbells (profiles/r03_rehearsal_n248.txt).
+__global__ void __launch_bounds__(64) door_wait_kernel(const unsigned long long* door, unsigned long long seq,
+                                                       unsigned long long spin_ticks, unsigned* err) {
+  if (threadIdx.x) return;
+  const unsigned long long t0 = rt_now();
+  for (unsigned k = 0; (__hip_atomic_load(door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & ~kCancelBit) < seq; ++k) {
+    __builtin_amdgcn_s_sleep(2);
+    if ((k & 255) == 255 && rt_now() - t0 > spin_ticks) {
+      __hip_atomic_fetch_or(err, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the message the doorbell released
+}
+
+hipError_t launch_door_wait(const unsigned long long* door, unsigned long long seq, unsigned long long spin_ticks,
+                            unsigned* err, hipStream_t s) {
+  hipLaunchKernelGGL(door_wait_kernel, dim3(1), dim3(64), 0, s, door, seq, spin_ticks, err);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Straggler emulation: a delayed worker's task runs on its own stream behind
+// this one-wave kernel, which starts once the worker's message has landed (stream order after
+// the exchange) and spins on s_memrealtime for the injected delay -- the reference worker's
+// sleep(rand()) between its Irecv and its reply (examples/iterative_example.jl:74,
+// test/kmap2.jl:95).  No host thread sits between the schedule and the latency the pool
+// records; one wave holds no CU anyone else needs.
+__global__ void __launch_bounds__(64) sleep_kernel(unsigned long long ticks) {
+  if (threadIdx.x) return;
+  const unsigned long long t0 = rt_now();
+  while (rt_now() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_sleep(unsigned long long ticks, hipStream_t s) {
+  hipLaunchKernelGGL(sleep_kernel, dim3(1), dim3(64), 0, s, ticks);
+  return hipGetLastError();
+}
+
 hipError_t launch_kmap(const KmapArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(kmap_task_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();

@@ -33,6 +33,17 @@ inline void dispatch(Pool& p, Comm& c, int64_t i, int64_t tag) {
   p.rreq_live[k] = 1;
 }
 
+// the gated replay's observation step (gate.cpp); a schedule that fails (kind mismatch,
+// over-release, timeout) closes the call first, as every other failure inside a call does
+inline void gate_step(Comm& c, int kind) {
+  try {
+    c.gate(kind);
+  } catch (...) {
+    c.end_call();
+    throw;
+  }
+}
+
 void check_comm(Pool& p, Comm* comm) {
   if (!comm) fail(MPA_ARGUMENT_ERROR, "comm is NULL");
   for (int64_t i = 0; i < p.n; ++i)
@@ -80,7 +91,7 @@ void asyncmap(Pool& p, const AsyncmapArgs& a) {
   c.begin_call(b);
 
   p.epoch = a.epoch;                                                               // :87
-  c.gate(MPA_GATE_CALL);  // gated replay: the completions phase 1's Test! may see (gate.cpp)
+  gate_step(c, MPA_GATE_CALL);  // gated replay: the completions phase 1's Test! may see (gate.cpp)
 
   for (int64_t i = 0; i < comm_size; ++i) {                                        // :91-114
     const size_t k = size_t(i);
@@ -122,7 +133,7 @@ void asyncmap(Pool& p, const AsyncmapArgs& a) {
     if (c.gated()) {  // the completions this Waitany! may see (a call that finds none live is MPI_UNDEFINED)
       bool live = false;
       for (int64_t j = 0; j < comm_size; ++j) live |= p.rreq_live[size_t(j)] != 0;
-      if (live) c.gate(MPA_GATE_WAIT);
+      if (live) gate_step(c, MPA_GATE_WAIT);
     }
     const int64_t i = c.waitany(comm_size, p.ranks.data(), p.rreq_live.data());   // :161
     if (i < 0) {  // MPI_UNDEFINED: undefined in the reference; an error here
@@ -166,7 +177,7 @@ void waitall(Pool& p, void* recvbuf, size_t recv_bytes, size_t recv_length, void
   b.rl = irecv_bytes / size_t(comm_size);
   b.n = comm_size;
   c.begin_call(b);
-  c.gate(MPA_GATE_WAITALL);
+  gate_step(c, MPA_GATE_WAITALL);
   c.waitall(comm_size, p.ranks.data(), p.rreq_live.data());                        // :212
   for (int64_t i = 0; i < comm_size; ++i) {                                        // :213-221
     const size_t k = size_t(i);

@@ -117,6 +117,13 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   // where a process serves one worker
   const char* arm = std::getenv("MPA_ARM");
   arm_mode_ = arm && *arm == '0' ? 0 : arm && *arm == '1' ? 1 : 2;
+  // how an armed task waits: one wave ahead of it (default) or every workgroup in-kernel
+  const char* dl = std::getenv("MPA_DELAY");
+  delay_on_device_ = dl && !std::strcmp(dl, "device");
+  const char* lead = std::getenv("MPA_DELAY_LEAD_NS");
+  if (lead) delay_lead_ns_ = std::atoll(lead);
+  const char* aw = std::getenv("MPA_ARM_WAIT");
+  arm_wave_ = !(aw && !std::strcmp(aw, "kernel"));
   const char* cb = measure_env("MPA_COORD_BATCH");
   coord_batches_ = !(cb && *cb == '0');
   fused_tail_ = !env_off("MPA_TAIL");
@@ -770,10 +777,20 @@ int64_t HipComm::counter(const char* name) const {
   if (k == "head_steps") return n_head_;    // epoch steps run at the head of a task launch
   if (k == "epoch_kernels") return n_epoch_;  // epoch steps run as their own epoch kernel
   if (k == "prearmed") return n_prearmed_;   // head steps whose launch was pre-armed
-  if (k == "stale_deferred") return n_deferred_;
-  if (k == "task_launches") return n_task_launches_.load(std::memory_order_relaxed);  // least-squares launches  // held re-dispatches whose messages joined the next step
+  if (k == "stale_deferred") return n_deferred_;  // held re-dispatches whose messages joined the next step
+  if (k == "task_launches") return n_task_launches_.load(std::memory_order_relaxed);  // least-squares launches
   if (k == "prearm_cancelled") return n_pre_cancel_;
   if (k == "prearm_same") return n_pre_same_;  // released with the step's predicted arguments
+  if (k == "armed") return n_armed_;  // server: tasks launched device-armed (some may be cancelled)
+  if (k == "sleeps") return n_sleeps_;  // delayed tasks: a sleep kernel ran before the task
+  if (k == "timer_late") return n_timer_late_.load(std::memory_order_relaxed);  // > 1 ms late timer launches
+  if (k == "queues") return queue_streams(dev_);  // CU-masked streams (HSA queues) the process holds
+  if (k == "shared_worker_streams") {  // workers whose stream another worker or comm also uses
+    int64_t k2 = 0;
+    for (const auto& w : w_)
+      if (w.stream && stream_shared(w.stream)) ++k2;
+    return k2;
+  }
   return -1;
 }
 

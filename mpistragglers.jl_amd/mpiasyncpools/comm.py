@@ -89,9 +89,10 @@ class _Comm:
         check(lib().mpa_comm_shutdown(self._h))
 
     def counter(self, name):
-        """An event counter of the transport (mpa_comm_counter): "held", "held_joined",
-        "held_alone", "gate_steps", "head_steps", "epoch_kernels", "prearmed", "prearm_cancelled",
-        "stale_deferred"; -1 if the transport does not count it."""
+        """An event counter of the transport (mpa_comm_counter, include/mpiasyncpools.h):
+        "held", "held_joined", "held_alone", "gate_steps", "head_steps", "epoch_kernels",
+        "prearmed", "prearm_cancelled", "prearm_same", "stale_deferred", "task_launches",
+        "armed", "sleeps", "timer_late", "queues", "shared_worker_streams"; -1 if the transport does not count it."""
         return int(lib().mpa_comm_counter(self._h, name.encode()))
 
     def set_gate(self, kinds, offsets, ranks):
@@ -108,6 +109,15 @@ class _Comm:
         self._keep["gate"] = (k, o, r)
         check(lib().mpa_comm_set_gate(self._h, int(k.size), k.ctypes.data if k.size else None,
                                       o.ctypes.data if o.size else None, r.ctypes.data if r.size else None))
+
+    def set_gate_clock(self, rank, done_ns):
+        """Paced gated replay (mpa_comm_set_gate_clock, HIP rank 0): the oracle's virtual
+        completion times of worker `rank`'s tasks 1.. (ns from the replay's first call); a
+        delayed task then completes at the replay's start + its time instead of `delay`
+        after its dispatch.  [] clears it."""
+        d = np.ascontiguousarray(done_ns, dtype=np.int64)
+        self._keep["gate_clock_%d" % rank] = d
+        check(lib().mpa_comm_set_gate_clock(self._h, int(rank), d.ctypes.data if d.size else None, int(d.size)))
 
     def _before_call(self, sendbuf):
         pass

@@ -13,6 +13,7 @@ lowest index, src/MPIAsyncPools.jl:161 over MPICH's array scan).
 import importlib.util
 import json
 import os
+import time
 
 import numpy as np
 
@@ -38,9 +39,27 @@ def oracle_gate(sc):
     return out, sim.gate_schedule(sc.get("ranks", list(range(1, n + 1))))
 
 
-def replay(M, sc, comm, buf, host, predicate):
+def gate_clock(sc):
+    """{comm rank: [virtual completion time of its task 1, 2, ...]} of a scenario on the
+    oracle's clock (mpa_comm_set_gate_clock: a paced replay)."""
+    mg = make_golden()
+    _, sim = mg.run_scenario(sc, return_sim=True)
+    ranks = sc.get("ranks", list(range(1, sc["n"] + 1)))
+    clock = {}
+    for w, t, post, done, seen in sorted(sim.events(), key=lambda e: (e[0], e[1])):
+        c = clock.setdefault(int(ranks[w]), [])
+        assert t == len(c) + 1, (w, t)
+        c.append(int(done))
+    return clock
+
+
+def replay(M, sc, comm, buf, host, predicate, snap=None):
     """Run a scenario's ops on the product through `comm`; the oracle's record layout.
-    `buf(k)` makes a float64 buffer of k elements, `host(b)` reads one back as numpy."""
+    `buf(k)` makes a float64 buffer of k elements, `host(b)` reads one back as numpy,
+    `snap(b)` (default: host) keeps a copy of recvbuf after each call -- a device clone, read
+    back after the last call, so the harness adds no host sync between calls (its time
+    between calls delays the next dispatch, which the oracle's coordinator does not)."""
+    snap = snap or host
     n = sc["n"]
     ranks = sc.get("ranks", list(range(1, n + 1)))
     pool = M.MPIAsyncPool(ranks, epoch0=sc.get("epoch0", 0), nwait=sc.get("default_nwait"))
@@ -49,6 +68,10 @@ def replay(M, sc, comm, buf, host, predicate):
     recv, irecv = buf(n * chunk), buf(n * chunk)
     out = []
     for op in sc["ops"]:
+        if op.get("advance_ns"):  # the coordinator's own time between calls (make_golden.py run_scenario)
+            t_end = time.perf_counter_ns() + int(op["advance_ns"])
+            while time.perf_counter_ns() < t_end:
+                pass
         if op["op"] == "waitall":
             M.waitall_(pool, recv, irecv)
         else:
@@ -58,7 +81,9 @@ def replay(M, sc, comm, buf, host, predicate):
             M.asyncmap_(pool, send, recv, isend, irecv, comm, nwait=nw, epoch=op.get("epoch"), tag=0)
         out.append({"repochs": pool.repochs.tolist(), "sepochs": pool.sepochs.tolist(),
                     "active": pool.active.astype(int).tolist(), "epoch": int(pool.epoch),
-                    "latency_s": pool.latency.tolist(), "recv": np.asarray(host(recv)).tolist()})
+                    "latency_s": pool.latency.tolist(), "recv": snap(recv)})
+    for r in out:
+        r["recv"] = np.asarray(host(r["recv"])).tolist()
     return out, pool
 
 
@@ -96,3 +121,19 @@ def random_scenario(seed):
         ops.append(op)
     d = rng.integers(0, 6, size=(n, 8)) * 1_000_000
     return {"name": f"rand{seed}", "n": n, "worker": "kmap2", "durations_ns": d.ravel().tolist(), "ops": ops}
+
+
+def warm_kernels(M, torch, n):
+    """Load the task / sleep / exchange code objects before a timing-sensitive trace (a
+    first launch loads its code object)."""
+    comm = M.DeviceComm(n)
+    for r in range(1, n + 1):
+        comm.set_task(r, "kmap2")
+        comm.set_delays(r, [1000, 0])
+    pool = M.MPIAsyncPool(n)
+    s = torch.zeros(1, dtype=torch.float64, device="cuda")
+    rb = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    for _ in range(3):
+        M.asyncmap_(pool, s, rb, torch.zeros(n, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), comm, nwait=n)
+    torch.cuda.synchronize()
+    comm.close()

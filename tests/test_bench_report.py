@@ -41,7 +41,10 @@ def test_contract_keys_and_throughput():
     assert r["measured_read_peak"] == 7200.0
     assert abs(r["frac_of_measured_read_peak"] - r["achieved"] / 7200.0) < 1e-3
     assert r["traffic"] is None or r["traffic"] > alg  # PMC file (profiles/) when present
-    assert r["timing_sample_period"] == 8 and "one in every 8 launches" in r["avg_launch_ms_source"]
+    # c2 times one launch in 8, lowered so that >= 16 launches are timed (100 steps: 1 in 6;
+    # the driver's 20-step line: every launch)
+    assert r["timing_sample_period"] == 6 and "one in every 6 launches" in r["avg_launch_ms_source"]
+    assert bench.timing_period(_args(steps=20), cfg) == 1 and bench.timing_period(_args(steps=300), cfg) == 8
     out5 = bench.report(_args(), _cfg("c5"), 1, 0.1, [(100, 60.0, 100 * alg, 60.0)], {})
     assert out5["roofline"]["timing_sample_period"] == 1 and "every launch" in out5["roofline"]["avg_launch_ms_source"]
 
@@ -50,12 +53,12 @@ def test_c1_samples_its_timing_events():
     """c1 (latency-bound) brackets one launch in 16 with the HIP events; --timing-period
     overrides it; the roofline says which."""
     cfg = _cfg("c1")
-    out = bench.report(_args(), cfg, 1, 0.1, [(7, 0.1, 7 * 6.4e6, 0.1)], {})
+    out = bench.report(_args(steps=3000), cfg, 1, 0.1, [(7, 0.1, 7 * 6.4e6, 0.1)], {})
     r = out["roofline"]
     assert r["timing_sample_period"] == 16 and "one in every 16 launches" in r["avg_launch_ms_source"]
     a = _args()
     a.timing_period = 1
-    assert bench.timing_period(a, cfg) == 1 and bench.timing_period(_args(), _cfg("c2")) == 8
+    assert bench.timing_period(a, cfg) == 1 and bench.timing_period(_args(steps=300), _cfg("c2")) == 8
 
 
 def test_multi_gpu_rate_is_per_gpu_average_and_no_traffic():

@@ -39,7 +39,8 @@ def _run_host(sc, seed=0):
     th.start()
     try:
         coord.set_gate(*sched)
-        got, pool = gated.replay(M, sc, coord, lambda k: np.zeros(k), lambda b: b, gated.make_golden().predicate)
+        got, pool = gated.replay(M, sc, coord, lambda k: np.zeros(k), lambda b: b, gated.make_golden().predicate,
+                                 snap=np.copy)
     finally:
         coord.shutdown()
         th.join(timeout=60)
@@ -90,7 +91,11 @@ def test_gate_errors():
     pool = M.MPIAsyncPool(2)
     with pytest.raises(M.ErrorException, match="gated replay"):
         M.asyncmap_(pool, np.zeros(1), np.zeros(6), np.zeros(2), np.zeros(6), coord, nwait=1)
+    # the failed step closed the call (pool.cpp gate_step): the comm serves the next call
     coord.set_gate([], [], [])
+    rep = M.asyncmap_(pool, np.zeros(1), np.zeros(6), np.zeros(2), np.zeros(6), coord, nwait=2)
+    assert rep.tolist() == [pool.epoch, pool.epoch] and not pool.active.any()
+    coord.shutdown()
     coord.close()
     sim = M.SimComm(2)
     with pytest.raises(M.ArgumentError):

@@ -92,10 +92,10 @@ def test_kmap2(M, torch_mod, nranks):
         delay = time.perf_counter() - t0
         assert repochs[0] == pool.epoch
         dev.append(abs(delay - pool.latency[0]))
-    # kmap2.jl:71 (atol 1e-3) at every call but at most two, which a host scheduling hiccup
-    # may delay by a few ms (1.5 ms once in round 3's runs); none beyond 5 ms
+    # kmap2.jl:71 (atol 1e-3) at every call (round 3 allowed two calls up to 5 ms: launches
+    # stalled on a process holding more HSA queues than the GPU maps, profiles/r04_gated_stall.txt)
     dev = np.sort(np.asarray(dev))
-    assert dev[-3] <= 1e-3 and dev[-1] <= 5e-3, dev[-5:]
+    assert dev[-1] <= 1e-3, dev[-5:]
     # t counts the tasks each worker served (kmap2.jl:82-84)
     M.waitall_(pool, recvbuf, irecvbuf)
     rb = recvbuf.cpu().numpy().reshape(nworkers, 3)
@@ -105,22 +105,38 @@ def test_kmap2(M, torch_mod, nranks):
 
 
 def _warm_kernels(M, torch, n):
-    """Load the task/delay/exchange code objects before a timing-sensitive trace."""
-    comm = M.DeviceComm(n)
-    for r in range(1, n + 1):
-        comm.set_task(r, "kmap2")
-        comm.set_delays(r, [1000, 0])
-    pool = M.MPIAsyncPool(n)
-    s = torch.zeros(1, dtype=torch.float64, device="cuda")
-    rb = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
-    for _ in range(3):
-        M.asyncmap_(pool, s, rb, torch.zeros(n, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), comm, nwait=n)
-    torch.cuda.synchronize()
-    comm.close()
+    import gated
+    gated.warm_kernels(M, torch, n)
+
+
+def test_queue_cap(M, torch_mod):
+    """The process holds at most MPA_MAX_QUEUES (12) CU-masked streams per device: a comm of
+    24 workers shares them, and a 9-worker comm after it gets a stream of its own per worker
+    (past ~20 queues the GPU time-slices them and launches stall ~10 ms,
+    profiles/r04_queue_latency.txt)."""
+    big = M.DeviceComm(24)
+    for r in range(1, 25):
+        big.set_task(r, "kmap2")
+    assert big.counter("queues") <= 12
+    assert big.counter("shared_worker_streams") >= 12
+    big.close()
+    c = M.DeviceComm(9)
+    for r in range(1, 10):
+        c.set_task(r, "kmap2")
+        c.set_delays(r, [1000])
+    assert c.counter("queues") <= 12 and c.counter("shared_worker_streams") == 0
+    pool = M.MPIAsyncPool(9)
+    torch = torch_mod
+    rb = torch.zeros(27, dtype=torch.float64, device="cuda")
+    M.asyncmap_(pool, torch.ones(1, dtype=torch.float64, device="cuda"), rb,
+                torch.zeros(9, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), c, nwait=9)
+    assert c.counter("sleeps") == 0 and c.counter("timer_late") == 0  # the host timer launched them
+    assert rb.cpu().numpy().reshape(9, 3)[:, 0].tolist() == list(range(1, 10))
+    c.close()
 
 
 def test_delay_calibration(M, torch_mod):
-    """An injected delay of d ms shows up as a latency of d ms (+ < 1 ms dispatch)."""
+    """An injected delay of d ms shows up as a latency of d ms (within 0.5 ms)."""
     torch = torch_mod
     _warm_kernels(M, torch, 2)
     comm = M.DeviceComm(2)
@@ -132,7 +148,8 @@ def test_delay_calibration(M, torch_mod):
     for _ in range(3):
         M.asyncmap_(pool, s, torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"),
                     comm, nwait=2)
-        assert 0.020 <= pool.latency[0] < 0.021 and 0.007 <= pool.latency[1] < 0.008, pool.latency
+        # the delay is dispatch -> reply (the task's ~35 us launch overhead is inside it)
+        assert abs(pool.latency[0] - 0.020) < 0.5e-3 and abs(pool.latency[1] - 0.007) < 0.5e-3, pool.latency
 
 
 def _lsq_case(M, torch, dtype, rows, cols, lda=None, seed=3, nworkers=1, grid=None):
@@ -429,10 +446,10 @@ def test_fused_head_matches_epoch_kernel(M, torch_mod, monkeypatch, dtype, cols)
     tdt = torch.float64 if dtype == "f64" else torch.float32
     A = _dev(torch, lsq.gen_matrix(seed, 0, n * rows, cols, dtype))
     b = _dev(torch, lsq.gen_vector(seed, 0, n * rows, dtype))
-    names = ("head_steps", "epoch_kernels", "prearmed", "prearm_cancelled")
+    names = ("head_steps", "epoch_kernels", "prearmed", "prearm_cancelled", "prearm_same")
 
     def run(nwait, **env):
-        for k in ("MPA_HEAD", "MPA_PREARM"):
+        for k in ("MPA_HEAD", "MPA_PREARM", "MPA_PRESAME"):
             monkeypatch.setenv(k, env.get(k, "1"))
         comm = M.DeviceComm(n)
         for r in range(1, n + 1):
@@ -466,11 +483,87 @@ def test_fused_head_matches_epoch_kernel(M, torch_mod, monkeypatch, dtype, cols)
     pre, s_pre = run(allf)
     nopre, s_nopre = run(allf, MPA_PREARM="0")
     assert s_pre["prearmed"] >= epochs - 3 and s_nopre["prearmed"] == 0, (s_pre, s_nopre)
+    # most pre-armed launches go with the step they predicted (kernel arguments, no mailbox
+    # read); with MPA_PRESAME=0 every one reads the mailbox: bitwise the same run
+    assert s_pre["prearm_same"] >= 1, s_pre
+    presame0, s_ps0 = run(allf, MPA_PRESAME="0")
+    assert s_ps0["prearm_same"] == 0 and s_ps0["prearmed"] >= epochs - 3, s_ps0
+    same(pre, presame0)
     same(pre, nopre)
     same(pre, on)
     part, s_part = run(n - 1)
     assert s_part["head_steps"] >= 1 and part[3] == epochs and max(part[4]) == epochs
     assert bool(torch.isfinite(part[0]).all()) and float(torch.linalg.norm(part[0])) > 0
+
+
+@pytest.mark.parametrize("rows4", [1024, 3072, 1 << 18], ids=["equal", "slow3x", "slow256x"])
+def test_native_k_of_n_prearmed_with_stragglers(M, torch_mod, monkeypatch, capfd, rows4):
+    """The native loop's shipped k-of-n fast path, ungated, at nwait 3 of 4: with equal shards
+    the epochs run in pre-armed launches (c1's pattern); with worker 4's shard 256x the
+    others' it replies late (a stale harvest inside a later call's wait loop,
+    src/MPIAsyncPools.jl:177-184), its re-dispatch is held and joins the next batched launch,
+    whose step runs at the head of the launch (3x: in between).  Whatever the timing,
+    the loop must compute what the reference's coordinator computes from the repochs it saw
+    (examples/iterative_example.jl:41-46): the iterate equals a torch fp64 replay of the
+    per-epoch repochs the loop traced (each chunk the gradient of the iterate sent at its
+    epoch, fresh chunks weighted 1), and each final chunk is the gradient of the iterate sent
+    at its repochs (1e-5, fp32).  The fast path did run: pre-armed launches (equal), held
+    re-dispatches and stale copies deferred into a step (256x)."""
+    import re
+    torch = torch_mod
+    monkeypatch.setenv("MPA_DESCENT_TRACE", "1")
+    monkeypatch.setenv("MPA_WAIT_TIMEOUT_S", "30")
+    n, nwait, cols, epochs, eta = 4, 3, 256, 80, 1e-4
+    rows = [1024, 1024, 1024, rows4]
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = [torch.randn(r, cols, device="cuda", generator=g) / cols ** 0.5 for r in rows]
+    b = [torch.randn(r, device="cuda", generator=g) for r in rows]
+    comm = M.DeviceComm(n)
+    for r in range(n):
+        comm.set_task_lsq(r + 1, A[r], b[r])
+    names = ("prearmed", "prearm_same", "held", "stale_deferred", "head_steps")
+    c0 = {k: comm.counter(k) for k in names}
+    pool = M.MPIAsyncPool(n)
+    x = torch.zeros(cols, device="cuda")
+    isend = torch.zeros(n * cols, device="cuda")
+    recv = torch.zeros(n * cols, device="cuda")
+    irecv = torch.zeros_like(recv)
+    capfd.readouterr()
+    M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, eta, epochs)
+    torch.cuda.synchronize()
+    err = capfd.readouterr().err
+    got = {k: comm.counter(k) - v for k, v in c0.items()}
+    trace = [list(map(int, m.group(1).split())) for m in re.finditer(r"\[mpa descent\] epoch \d+ repochs ([\d ]+) \|", err)]
+    assert len(trace) == epochs, (len(trace), err[-500:])
+    A64 = [a.double() for a in A]
+    b64 = [v.double() for v in b]
+
+    def grad(i, xv):
+        return A64[i].T @ (A64[i] @ xv - b64[i])
+
+    xs = [torch.zeros(cols, dtype=torch.float64, device="cuda")]  # xs[e-1]: the iterate sent at epoch e
+    for e, rep in enumerate(trace, start=1):
+        fresh = [i for i in range(n) if rep[i] == e]
+        assert len(fresh) >= nwait, (e, rep)
+        upd = sum(grad(i, xs[e - 1]) for i in fresh) * (n / len(fresh))
+        xs.append(xs[e - 1] - eta * upd)
+    rel = float(torch.linalg.norm(x.double() - xs[-1]) / torch.linalg.norm(xs[-1]))
+    assert rel <= 1e-5, rel
+    M.waitall_(pool, recv, irecv)
+    torch.cuda.synchronize()
+    ch = recv.view(n, cols).double()
+    for i in range(n):
+        r = int(pool.repochs[i])
+        ref = grad(i, xs[r - 1])
+        assert float(torch.linalg.norm(ch[i] - ref) / torch.linalg.norm(ref)) <= 1e-5, i
+    stale = sum(1 for e, rep in enumerate(trace, start=1) if rep[3] not in (0, e))
+    print("k-of-n native rows4=%d: %s, epochs with worker 4 stale %d of %d, iterate rel %.2e"
+          % (rows4, got, stale, epochs, rel))
+    if rows4 == rows[0]:
+        assert got["prearmed"] >= 1, got
+    if rows4 == 1 << 18:
+        assert got["held"] >= 1 and got["stale_deferred"] >= 1, got
+    comm.close()
 
 
 def test_read_bandwidth_probe(M, torch_mod):

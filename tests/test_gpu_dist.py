@@ -63,7 +63,43 @@ def test_lsqb_two_processes(built, monkeypatch, arm, cols):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     monkeypatch.setenv("MPA_ARM", arm)
-    _run(dist_worker.lsqb_dist, 2, [0, 1], cols)
+    _run(dist_worker.lsqb_dist, 2, [0, 1], cols, arm == "2")
+
+
+# ---- the N = 8 placement (one worker per process) on ONE GPU --------------------------------
+# On the node each worker process has a GPU of its own; here all eight share GPU 0.  The
+# default arms every worker process's next task behind a one-wave doorbell wait
+# (door_wait_kernel), so seven waiting tasks hold seven waves, not seven launch grids
+# (round 3's in-kernel wait timed out here, profiles/r03_rehearsal_n248.txt).
+
+def test_lsq_descent_eight_processes_armed(built):
+    """BASELINE c2's N = 8 placement (rank 0 coordinates and serves worker 1, ranks 1-7 one
+    worker each, device-armed by default): the native loop's iterate, replies and messages
+    bitwise equal to the one-process Python loop on the same shards, and every server
+    armed its tasks."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.lsq_descent_dist, 8, list(range(8)), {"MPA_TEST_EXPECT_ARMED": "1"}, timeout=240)
+
+
+def test_lsq_descent_eight_processes_host_launched(built):
+    """The same with MPA_ARM=0 (the serve loops launch each task when they see its doorbell)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.lsq_descent_dist, 8, list(range(8)), {"MPA_ARM": "0", "MPA_TEST_EXPECT_ARMED": "0"}, timeout=240)
+
+
+def test_lsqb_eight_processes_armed(built, monkeypatch):
+    """BASELINE c5's N = 8 placement: the batched 64-iterate task at 2048 columns (lsqp4's
+    FULL form) in eight processes, every server device-armed, every G against the fp64
+    oracle at 1e-5."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.delenv("MPA_ARM", raising=False)
+    _run(dist_worker.lsqb_dist, 8, list(range(8)), 2048, True, timeout=240)
 
 
 @pytest.mark.parametrize("placement,env", [

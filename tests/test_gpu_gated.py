@@ -38,6 +38,7 @@ def M(built):
     if not torch.cuda.is_available():
         pytest.skip("no GPU visible")
     import mpiasyncpools
+    gated.warm_kernels(mpiasyncpools, torch, 4)
     return mpiasyncpools
 
 
@@ -54,7 +55,8 @@ def _kmap2_run(M, sc, delays):
 
     def buf(k):
         return torch.zeros(k, dtype=torch.float64, device="cuda")
-    got, pool = gated.replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), gated.make_golden().predicate)
+    got, pool = gated.replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), gated.make_golden().predicate,
+                             snap=lambda t: t.clone())
     comm.shutdown()
     comm.close()
     return got
@@ -63,9 +65,10 @@ def _kmap2_run(M, sc, delays):
 @pytest.mark.parametrize("name", [s["name"] for s in SCEN])
 def test_golden_scenario_gated_on_device(M, name):
     """Every golden scenario at its committed durations: bit-exact trace; latency (host time,
-    dispatch -> harvest) within 10 ms of the oracle's virtual latency at every call but at most
-    one (within 50 ms), and within 3 ms at the median (timer wake-ups and coordinator time move it; the gate, not
-    the latency, pins the order)."""
+    dispatch -> harvest, src/MPIAsyncPools.jl:105,164,215) within 1 ms of the oracle's virtual
+    latency at every harvest (test/kmap2.jl:71's atol).  Round 3 allowed one 10-50 ms outlier:
+    launches stalled while the process held more HSA queues than the GPU maps
+    (profiles/r04_gated_stall.txt); the process now holds at most 12."""
     sc = next(s for s in SCEN if s["name"] == name)
     comm_n = sc.get("comm_workers", sc["n"])
     dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(comm_n, -1)
@@ -78,9 +81,7 @@ def test_golden_scenario_gated_on_device(M, name):
                 dev.append(abs(v - lat / 1e9))
     dev = np.asarray(dev)
     print("%s: latency |device - oracle| median %.3f ms, max %.3f ms" % (name, 1e3 * np.median(dev), 1e3 * dev.max()))
-    # one late timer wake-up (a host scheduling hiccup: 16.8 ms once in round 3, every other
-    # call within 0.1 ms, the trace bit-exact) may exceed the 10 ms bound, not two
-    assert np.sort(dev)[-2 if dev.size > 1 else -1] < 10e-3 and dev.max() < 50e-3 and np.median(dev) < 3e-3
+    assert dev.max() <= 1e-3 and np.median(dev) < 0.2e-3
 
 
 @pytest.mark.parametrize("seed", range(6))
