@@ -312,10 +312,6 @@ int mpa_comm_set_gate(mpa_comm* comm, int64_t nsteps, const int* kinds, const in
   return guarded([&] { comm_of(comm).set_gate(kinds, offsets, ranks, nsteps); });
 }
 
-int mpa_comm_set_gate_clock(mpa_comm* comm, int64_t rank, const int64_t* done_ns, int64_t count) {
-  return guarded([&] { comm_of(comm).set_gate_clock(rank, done_ns, count); });
-}
-
 int64_t mpa_comm_counter(mpa_comm* comm, const char* name) {
   int64_t r = -1;
   const int rc = guarded([&] {

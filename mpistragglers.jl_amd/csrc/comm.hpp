@@ -88,15 +88,6 @@ class Comm {
   // After the last step the next observation switches the gate off.
   void set_gate(const int* kinds, const int64_t* offsets, const int64_t* ranks, int64_t nsteps);
   void gate(int kind);
-  // paced replay (mpa_comm_set_gate_clock): worker `rank`'s tasks 1..count complete at the
-  // virtual times done_ns (ns from the gate's first step); gate_due() is the host time a
-  // delayed task `seq` of `rank` should complete at, or 0 if the schedule does not say
-  void set_gate_clock(int64_t rank, const int64_t* done_ns, int64_t count);
-  uint64_t gate_due(int64_t rank, uint64_t seq) const {
-    if (!gate_on_ || !gate_t0_ || size_t(rank - 1) >= gate_clock_.size()) return 0;
-    const auto& c = gate_clock_[size_t(rank - 1)];
-    return seq >= 1 && seq <= c.size() && c[seq - 1] >= 0 ? gate_t0_ + uint64_t(c[seq - 1]) : 0;
-  }
   bool gated() const { return gate_on_; }
   size_t gate_steps_taken() const { return gate_step_; }
 
@@ -125,8 +116,6 @@ class Comm {
   std::vector<int> gate_kinds_;
   std::vector<int64_t> gate_off_, gate_ranks_;
   std::vector<uint64_t> gate_rel_;  // completions released per worker
-  std::vector<std::vector<int64_t>> gate_clock_;  // virtual completion times per worker task
-  uint64_t gate_t0_ = 0;                          // host time of the first step (virtual 0)
 };
 
 Comm* make_sim_comm(int64_t nworkers);

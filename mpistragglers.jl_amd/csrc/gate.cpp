@@ -44,16 +44,7 @@ void Comm::set_gate(const int* kinds, const int64_t* offsets, const int64_t* ran
   gate_rel_.assign(size_t(nworkers_), 0);
   for (int64_t r = 1; r <= nworkers_; ++r) gate_rel_[size_t(r - 1)] = gate_posted(r);
   gate_step_ = 0;
-  gate_t0_ = 0;
   gate_on_ = true;
-}
-
-void Comm::set_gate_clock(int64_t rank, const int64_t* done_ns, int64_t count) {
-  if (!gate_supported()) fail(MPA_ARGUMENT_ERROR, "this transport has no gated replay (HIP and HOST rank 0 do)");
-  if (rank < 1 || rank > nworkers_) fail(MPA_ARGUMENT_ERROR, "gate clock: rank %lld is not a worker rank", (long long)rank);
-  if (count < 0 || (count > 0 && !done_ns)) fail(MPA_ARGUMENT_ERROR, "bad gate clock");
-  if (gate_clock_.size() < size_t(nworkers_)) gate_clock_.resize(size_t(nworkers_));
-  gate_clock_[size_t(rank - 1)].assign(done_ns, done_ns + count);
 }
 
 void Comm::gate(int kind) {
@@ -62,7 +53,6 @@ void Comm::gate(int kind) {
     gate_on_ = false;
     return;
   }
-  if (gate_step_ == 0) gate_t0_ = now_ns();  // the replay's virtual time 0
   if (gate_kinds_[gate_step_] != kind)
     fail(MPA_ERROR, "gated replay: step %zu of the schedule is a %s observation, the state machine is at a %s",
          gate_step_, gate_kind_name(gate_kinds_[gate_step_]), gate_kind_name(kind));

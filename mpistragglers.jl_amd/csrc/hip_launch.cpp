@@ -297,9 +297,7 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
     // overhead is taken out of the sleep (delay_lead_ns_), or it would accumulate along every
     // worker's chain of tasks: the gated kmap2_n9 replay drifted 1.2-1.9 ms from the
     // oracle's latencies by its 100th call with 40 us per task (profiles/r04_gated_stall.txt).
-    int64_t sleep_ns = delay - delay_lead_ns_;
-    // a paced gated replay: complete when the oracle's clock says (mpa_comm_set_gate_clock)
-    if (const uint64_t due = delay > 0 ? gate_due(rank, w.seq) : 0) sleep_ns = int64_t(due) - int64_t(mono_ns()) - delay_lead_ns_;
+    const int64_t sleep_ns = delay - delay_lead_ns_;
     if (sleep_ns > 0 && delay_on_device_) {
       HIPCHECK(launch_sleep((unsigned long long)(double(sleep_ns) * rt_hz_ / 1e9), s));
       n_sleeps_ += 1;
@@ -764,7 +762,8 @@ void HipComm::enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int
                   : b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #else
   // the product carries the iterate-halves single pass and the two passes only
-  HIPCHECK(b.pair ? launch_lsqp4(b.halves, s) : launch_lsqb(b.two, s));
+  static const bool p5 = [] { const char* e = std::getenv("MPA_LSQP5"); return e && *e == '1'; }();
+  HIPCHECK(b.pair ? (p5 ? launch_lsqp5(b.halves, s) : launch_lsqp4(b.halves, s)) : launch_lsqb(b.two, s));
 #endif
   if (timed) {
     HIPCHECK(hipEventRecord(tl.stop, s));

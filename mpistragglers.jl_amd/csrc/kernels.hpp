@@ -274,6 +274,8 @@ struct LsqpBatch {
 hipError_t launch_lsqp(const LsqpBatch& a, hipStream_t s);
 // the same batch by the one-wave-per-SIMD cut (lsqp4_kernel.hip, the default)
 hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s);
+// the same with phase 2 as 32x32x16 MFMAs (lsqp5_kernel.hip)
+hipError_t launch_lsqp5(const LsqpBatch& a, hipStream_t s);
 // Single pass by COLUMN pairs (lsqc_kernel.hip): the two members of a row group split the
 // columns (member h: columns 1024 h .. 1024 h + 1023), each holding all 64 iterates of its G
 // columns, and exchange their 16 x 64 partial products per 16-row block as tagged granules.

@@ -9,7 +9,7 @@ drift apart.
 """
 import re
 
-ABI_VERSION = 4
+ABI_VERSION = 3
 
 # one C prototype per entry point, exactly as include/mpiasyncpools.h declares it
 PROTOTYPES = """
@@ -42,7 +42,6 @@ int mpa_comm_set_delays(mpa_comm* comm, int64_t rank, const int64_t* delays_ns, 
 int64_t mpa_comm_tasks_done(mpa_comm* comm, int64_t rank);
 int mpa_comm_shutdown(mpa_comm* comm);
 int mpa_comm_set_gate(mpa_comm* comm, int64_t nsteps, const int* kinds, const int64_t* offsets, const int64_t* ranks);
-int mpa_comm_set_gate_clock(mpa_comm* comm, int64_t rank, const int64_t* done_ns, int64_t count);
 int64_t mpa_comm_counter(mpa_comm* comm, const char* name);
 int mpa_comm_create_dist(int transport, int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg_bytes, mpa_comm** out);
 int mpa_comm_serve(mpa_comm* comm);

@@ -110,15 +110,6 @@ class _Comm:
         check(lib().mpa_comm_set_gate(self._h, int(k.size), k.ctypes.data if k.size else None,
                                       o.ctypes.data if o.size else None, r.ctypes.data if r.size else None))
 
-    def set_gate_clock(self, rank, done_ns):
-        """Paced gated replay (mpa_comm_set_gate_clock, HIP rank 0): the oracle's virtual
-        completion times of worker `rank`'s tasks 1.. (ns from the replay's first call); a
-        delayed task then completes at the replay's start + its time instead of `delay`
-        after its dispatch.  [] clears it."""
-        d = np.ascontiguousarray(done_ns, dtype=np.int64)
-        self._keep["gate_clock_%d" % rank] = d
-        check(lib().mpa_comm_set_gate_clock(self._h, int(rank), d.ctypes.data if d.size else None, int(d.size)))
-
     def _before_call(self, sendbuf):
         pass
 

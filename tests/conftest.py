@@ -22,3 +22,13 @@ def built():
     if not os.path.exists(os.path.join(ROOT, "mpistragglers.jl_amd", "_build", "libmpiasyncpools.so")):
         subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "mpistragglers.jl_amd")])
     return True
+
+
+@pytest.fixture(autouse=True)
+def _release_comms(request):
+    """After a GPU test, collect the comms it left unclosed: their streams go back to the
+    process's capped queue set (MPA_MAX_QUEUES), or the next comm's workers would share them."""
+    yield
+    if request.node.get_closest_marker("gpu"):
+        import gc
+        gc.collect()

@@ -1,5 +1,5 @@
 """Per-rank bodies of the multi-process tests (spawned by tests/test_dist_cpu.py and
-tests/test_gpu_dist.py).  Rank 0 is the coordinator; the other ranks serve the workers
+tests/test_gpu_procs.py).  Rank 0 is the coordinator; the other ranks serve the workers
 placed on them.  Mirrors test/kmap2.jl with the workers spread over processes (as the
 reference's MPI ranks are) instead of living in the coordinator's process."""
 import os

@@ -44,7 +44,7 @@ def test_library_exports_every_declared_symbol(built):
 
 def test_abi_version_and_build_info(built):
     from mpiasyncpools._capi import lib
-    assert lib().mpa_abi_version() == 4
+    assert lib().mpa_abi_version() == 3
     assert b"gfx950" in lib().mpa_build_info()
 
 

@@ -1,6 +1,10 @@
-"""The multi-process HIP transport on a GPU box: rank 0 coordinates, rank 1 (a second
-process on the same GPU) serves workers through the shared-memory mailboxes; kmap2.jl
-properties across processes and a least-squares epoch checked against the fp64 oracle."""
+"""The multi-process HIP transport on a GPU box: rank 0 coordinates, ranks 1.. (other
+processes on the same GPU) serve workers through the shared-memory mailboxes; kmap2.jl
+properties across processes and least-squares epochs checked against the fp64 oracle.
+
+(Named to run after the single-process GPU tests: in round 4 the gated replays' latencies
+were disturbed for about a minute after the eight-process tests had run and exited,
+profiles/r04_gated_stall.txt.)"""
 import multiprocessing as mp
 import random
 

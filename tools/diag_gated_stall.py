@@ -52,6 +52,7 @@ def run(sc):
     comm.shutdown()
     comm.close()
     bad = gated.mismatches(sc["name"], got, sc["results"])
+    tol = gated.latency_tolerance(sc)
     dev, where = [], []
     for k, (g, r) in enumerate(zip(got, sc["results"])):
         for i, (v, lat) in enumerate(zip(g["latency_s"], r["latency_ns"])):
@@ -60,6 +61,8 @@ def run(sc):
                 where.append((k, i))
     dev = np.asarray(dev)
     big = [(where[j], round(1e3 * dev[j], 2)) for j in np.argsort(dev)[::-1][:4] if dev[j] > 0.5e-3]
+    over = [(where[j], round(1e3 * dev[j], 2), round(1e3 * tol[where[j]], 2)) for j in range(len(dev)) if dev[j] > tol[where[j]]]
+    print("    beyond tolerance: %d %s" % (len(over), over[:5]))
     for j in np.argsort(dev)[::-1][:3]:
         k, i = where[j]
         print("    op %d %s worker %d: oracle %.3f ms device %.3f ms" % (

@@ -15,6 +15,7 @@
 #   trace:CFG[:ARGS]             rocprofv3 --kernel-trace --stats of that bench -> trace_CFG/
 #   pmc:CFG:CTRS[:ARGS]          one rocprofv3 --pmc pass (CTRS comma-separated) -> pmc_CFG_<n>/
 #   ab:CFG:REPS:LIB[:ARGS]       REPS alternations: product library, then MPA_LIB=LIB (A/B on one box)
+#   abenv:CFG:REPS:VAR=VAL[:ARGS] REPS alternations: default environment, then VAR=VAL
 #   py:SCRIPT[:ARGS]             python tools/SCRIPT ARGS -> SCRIPT.log
 #   probe:BIN[:ARGS]             tools/bin/BIN ARGS -> BIN.txt
 set -u
@@ -41,9 +42,9 @@ run_step() {
     tests)
       local k=()
       [ -n "$a" ] && k=(-k "${a//+/ }")
-      timeout -k 10 1500 python -u -m pytest tests -m gpu -v -rP --timeout 240 --timeout-method thread "${k[@]}" > "$O/tests.log" 2>&1
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -v -rP --timeout 240 --timeout-method thread "${k[@]}" > "$O/tests${TESTS_TAG:-}.log" 2>&1
       local rc=$?
-      grep -E "^(FAILED|ERROR)|passed|failed" "$O/tests.log" | tail -5
+      grep -E "^(FAILED|ERROR)|passed|failed" "$O/tests${TESTS_TAG:-}.log" | tail -5
       return $rc ;;
     bench)
       timeout -k 10 600 python -u bench.py --config "$a" ${b//+/ } > "$O/bench_$a.log" 2>&1 || { r=$?; tail -20 "$O/bench_$a.log"; return $r; }
@@ -63,6 +64,14 @@ run_step() {
         echo "  A $i $(grep '^{' "$O/ab_${a}_A$i.log" | python3 -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('avg_launch_ms'))")"
         MPA_LIB="$c" timeout -k 10 600 python -u bench.py --config "$a" --no-cpu-baseline ${d//+/ } > "$O/ab_${a}_B$i.log" 2>&1 || { r=$?; tail -20 "$O/ab_${a}_B$i.log"; return $r; }
         echo "  B $i $(grep '^{' "$O/ab_${a}_B$i.log" | python3 -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('avg_launch_ms'))")"
+      done ;;
+    abenv)
+      local i
+      for i in $(seq 1 "$b"); do
+        timeout -k 10 600 python -u bench.py --config "$a" --no-cpu-baseline ${d//+/ } > "$O/abenv_${a}_A$i.log" 2>&1 || { r=$?; tail -20 "$O/abenv_${a}_A$i.log"; return $r; }
+        echo "  A $i $(grep '^{' "$O/abenv_${a}_A$i.log" | python3 -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('avg_launch_ms'), (d.get('roofline') or {}).get('frac'))")"
+        env "$c" timeout -k 10 600 python -u bench.py --config "$a" --no-cpu-baseline ${d//+/ } > "$O/abenv_${a}_B$i.log" 2>&1 || { r=$?; tail -20 "$O/abenv_${a}_B$i.log"; return $r; }
+        echo "  B $i $(grep '^{' "$O/abenv_${a}_B$i.log" | python3 -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('avg_launch_ms'), (d.get('roofline') or {}).get('frac'))")"
       done ;;
     py)
       timeout -k 10 600 python -u "tools/$a" ${b//+/ } > "$O/${a%.py}.log" 2>&1 || { r=$?; tail -20 "$O/${a%.py}.log"; return $r; }
