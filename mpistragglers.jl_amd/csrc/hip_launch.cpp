@@ -758,12 +758,13 @@ void HipComm::enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int
     HIPCHECK(hipEventRecord(tl.start, s));
   }
 #if MPA_MEASURE
-  HIPCHECK(b.pair ? (b.cpair ? launch_lsqc(b.halves, s) : b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
+  static const bool p5 = [] { const char* e = measure_env("MPA_LSQP5"); return e && *e == '1'; }();
+  HIPCHECK(b.pair ? (b.cpair ? launch_lsqc(b.halves, s) : b.pair8 ? launch_lsqp(b.halves, s)
+                             : p5 ? launch_lsqp5(b.halves, s) : launch_lsqp4(b.halves, s))
                   : b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #else
   // the product carries the iterate-halves single pass and the two passes only
-  static const bool p5 = [] { const char* e = std::getenv("MPA_LSQP5"); return e && *e == '1'; }();
-  HIPCHECK(b.pair ? (p5 ? launch_lsqp5(b.halves, s) : launch_lsqp4(b.halves, s)) : launch_lsqb(b.two, s));
+  HIPCHECK(b.pair ? launch_lsqp4(b.halves, s) : launch_lsqb(b.two, s));
 #endif
   if (timed) {
     HIPCHECK(hipEventRecord(tl.stop, s));

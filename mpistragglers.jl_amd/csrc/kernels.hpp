@@ -274,7 +274,8 @@ struct LsqpBatch {
 hipError_t launch_lsqp(const LsqpBatch& a, hipStream_t s);
 // the same batch by the one-wave-per-SIMD cut (lsqp4_kernel.hip, the default)
 hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s);
-// the same with phase 2 as 32x32x16 MFMAs (lsqp5_kernel.hip)
+// the same with phase 2 as 32x32x16 MFMAs (measure/lsqp5_kernel.hip, measurement build: MPA_LSQP5=1;
+// fewer instructions, the same time: DESIGN.md §10)
 hipError_t launch_lsqp5(const LsqpBatch& a, hipStream_t s);
 // Single pass by COLUMN pairs (lsqc_kernel.hip): the two members of a row group split the
 // columns (member h: columns 1024 h .. 1024 h + 1023), each holding all 64 iterates of its G

@@ -73,9 +73,6 @@ constexpr int PF = 4;                 // G tree fan-in
 #ifndef MPA_LSQP4_P2L
 #define MPA_LSQP4_P2L 1               // phase-2 transposed-read chunks in flight ahead (1 vs 2: -1 %, r02_c5_strip_ring.txt)
 #endif
-#ifndef MPA_LSQP4_P1C
-#define MPA_LSQP4_P1C 2               // phase-1 accumulator chains (2: one per iterate tile; 4: x k parity)
-#endif
 #ifndef MPA_LSQP4_AD
 #define MPA_LSQP4_AD 3                // phase-1 fragment read-ahead in k-steps (3 beats 2, 4, 6)
 #endif
@@ -465,28 +462,12 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     };
 #pragma unroll
     for (int s = 0; s < AD; ++s) af[s] = rd1(s);
-#if MPA_LSQP4_P1C == 4
-    // four accumulator chains (iterate tile x k-step parity): a chain's next MFMA is four MFMAs
-    // later instead of two, so no MFMA waits for its own previous result
-    f32x4 p1o[2];
-#endif
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       __builtin_amdgcn_sched_barrier(0);
       if (s + AD < NKS && ((s + AD) & 1) == 0) wait_strip((s + AD) / 2);
 #if MPA_LSQP4_PROBE & 4
       (void)af;
-#elif MPA_LSQP4_VACC && MPA_LSQP4_P1C == 4
-      if (s == 1) {
-        p1o[0] = mfma_v0(af[s % AD], XF[s][0]);
-        p1o[1] = mfma_v0(af[s % AD], XF[s][1]);
-      } else if (s & 1) {
-        mfma_v(p1o[0], af[s % AD], XF[s][0]);
-        mfma_v(p1o[1], af[s % AD], XF[s][1]);
-      } else {
-        mfma_v(p1[0], af[s % AD], XF[s][0]);
-        mfma_v(p1[1], af[s % AD], XF[s][1]);
-      }
 #elif MPA_LSQP4_VACC
       mfma_v(p1[0], af[s % AD], XF[s][0]);
       mfma_v(p1[1], af[s % AD], XF[s][1]);
@@ -499,11 +480,6 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     __builtin_amdgcn_sched_barrier(0);
 #if MPA_LSQP4_VACC
     mfma_v_settle(p1[0], p1[1]);
-#if MPA_LSQP4_P1C == 4
-    mfma_v_settle(p1o[0], p1o[1]);
-    p1[0] += p1o[0];
-    p1[1] += p1o[1];
-#endif
 #endif
     }
     // phase 2's column tiles in chunks of 4 = one strip (8 transposed reads), double-buffered:
