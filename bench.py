@@ -512,13 +512,10 @@ def run_multi(args, cfg, rank, world, local):
     import mpiasyncpools as M
 
     # MPA_BENCH_ONE_GPU=1 rehearses the N-process path with every rank on GPU 0 (1-GPU box).
-    # There the device-armed tasks of processes serving one worker (N = 8) spin on CUs and queue
-    # slots of the very GPU that has to run rank 0's step that rings their doorbells: they can
-    # only time out (profiles/r03_rehearsal_n248.txt), so the rehearsal host-launches unless told
-    # otherwise; on the node each of those processes has a GPU of its own
+    # Round 3's device-armed tasks waited in every workgroup and could only time out there (their
+    # grids held the CUs rank 0's step needed, profiles/r03_rehearsal_n248.txt); an armed task now
+    # waits behind one wave (door_wait_kernel), so the rehearsal runs the node's default path too
     one_gpu = os.environ.get("MPA_BENCH_ONE_GPU") == "1"
-    if one_gpu:
-        os.environ.setdefault("MPA_ARM", "0")
     torch.cuda.set_device(0 if one_gpu else local)
     dist.init_process_group("gloo")
     n = cfg["workers"]
