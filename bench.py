@@ -338,8 +338,8 @@ def report(args, cfg, world, el, per_rank, extra):
     return out
 
 
-ROCPROF_STATS = {"c2": ("r03_c2_kernel_stats.csv", "lsq_grad_kernel"),
-                 "c5": ("r03_c5_kernel_stats.csv", "lsqp4_kernel")}
+ROCPROF_STATS = {"c2": ("r04_c2_kernel_stats.csv", "lsq_grad_kernel"),
+                 "c5": ("r04_c5_kernel_stats.csv", "lsqp4_kernel")}
 
 
 def rocprof_avg_ms(cfg):
@@ -348,7 +348,7 @@ def rocprof_avg_ms(cfg):
     (tools/trace_window.py) of the newest round that has one, else the --stats summary; None
     without either."""
     name, kernel = ROCPROF_STATS.get(cfg["config"], (None, None))
-    for rnd in ("r03", "r02"):
+    for rnd in ("r04", "r03", "r02"):
         win = os.path.join(ROOT, "profiles", "%s_%s_rocprof_window.json" % (rnd, cfg["config"]))
         if name and os.path.exists(win):
             d = json.load(open(win))
