@@ -257,3 +257,56 @@ def test_lsqp4_full_form_matches_general_form_bitwise(M):
         assert np.array_equal(out_f[i].view(np.uint32), out_g[i].view(np.uint32)), i
     err = lsq.rel_err(out_g[2], lsq.batched_shard_gradient(shards_g[2][0], shards_g[2][1], X, "bf16"))
     assert err <= TOL, err
+
+
+_VARIANT_CHILD = r"""
+import os, sys
+import numpy as np
+sys.path[:0] = [os.path.join(sys.argv[1], p) for p in ("tests", "mpistragglers.jl_amd", "oracle")]
+import torch
+import mpiasyncpools as M
+import test_gpu_lsqb as T
+outs = []
+for rows, cols, n, seed in T._VARIANT_CASES:
+    A, B, X = T._problem(n * rows, cols, seed)
+    shards = [(A[i * rows:(i + 1) * rows - (i if rows % 16 else 0)], B[i * rows:(i + 1) * rows - (i if rows % 16 else 0)])
+              for i in range(n)]
+    out, rep, comm, _ = T._run(M, torch, shards, cols, X)
+    comm.close()
+    outs.append(out)
+np.savez(sys.argv[2], *outs)
+"""
+_VARIANT_CASES = [(4800, 2048, 2, 91), (3001, 2048, 3, 92), (2500, 1312, 2, 93)]
+
+
+@pytest.mark.parametrize("var", ["MPA_LSQP6"])
+def test_pipelined_variant_matches_lsqp4_bitwise(M, tmp_path, var):
+    """The software-pipelined c5 kernel (measure/lsqp6_kernel.hip, measurement build,
+    MPA_LSQP6=1: phase 1 of block v beside phase 2 of block v - 1) sums in lsqp4's order (the
+    -B MFMA, k-steps in order, the same reduce, the blocks in order; block -1 adds an exact
+    +0), so its G equals lsqp4's bit for bit, FULL (cols 2048, rows % 16 = 0) and general form.
+    The variant is chosen once per process (a static read of the environment): it runs in a
+    child process on the same inputs."""
+    import os
+    import subprocess
+    import sys
+    import torch
+    if b"measurement build" not in M.lib().mpa_build_info():
+        pytest.skip("a c5 variant of the measurement build (make MEASURE=1, MPA_LIB=...): not in the product")
+    if os.environ.get(var):
+        pytest.skip(f"{var} is set for this process: lsqp4 is not the in-process kernel")
+    mine = []
+    for rows, cols, n, seed in _VARIANT_CASES:
+        A, B, X = _problem(n * rows, cols, seed)
+        shards = [(A[i * rows:(i + 1) * rows - (i if rows % 16 else 0)], B[i * rows:(i + 1) * rows - (i if rows % 16 else 0)])
+                  for i in range(n)]
+        out, rep, comm, _ = _run(M, torch, shards, cols, X)
+        comm.close()
+        mine.append(out)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dst = str(tmp_path / "variant.npz")
+    env = dict(os.environ, **{var: "1"})
+    subprocess.run([sys.executable, "-c", _VARIANT_CHILD, root, dst], env=env, check=True, timeout=180)
+    theirs = np.load(dst)
+    for k, out in enumerate(mine):
+        assert np.array_equal(out.view(np.uint32), theirs[f"arr_{k}"].view(np.uint32)), _VARIANT_CASES[k]

@@ -16,6 +16,7 @@
 #   pmc:CFG:CTRS[:ARGS]          one rocprofv3 --pmc pass (CTRS comma-separated) -> pmc_CFG_<n>/
 #   ab:CFG:REPS:LIB[:ARGS]       REPS alternations: product library, then MPA_LIB=LIB (A/B on one box)
 #   abenv:CFG:REPS:VAR=VAL[:ARGS] REPS alternations: default environment, then VAR=VAL
+#   var:NAME:CFG:V=X,V=Y[:ARGS]  python bench.py --config CFG ARGS under V=X V=Y -> var_NAME.log
 #   py:SCRIPT[:ARGS]             python tools/SCRIPT ARGS -> SCRIPT.log
 #   probe:BIN[:ARGS]             tools/bin/BIN ARGS -> BIN.txt
 set -u
@@ -73,6 +74,12 @@ run_step() {
         env "$c" timeout -k 10 600 python -u bench.py --config "$a" --no-cpu-baseline ${d//+/ } > "$O/abenv_${a}_B$i.log" 2>&1 || { r=$?; tail -20 "$O/abenv_${a}_B$i.log"; return $r; }
         echo "  B $i $(grep '^{' "$O/abenv_${a}_B$i.log" | python3 -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('avg_launch_ms'), (d.get('roofline') or {}).get('frac'))")"
       done ;;
+    var)
+      # var:NAME:CFG:VAR=VAL,VAR=VAL[:ARGS]  one bench under extra environment -> var_NAME.log
+      local envs=()
+      IFS=',' read -r -a envs <<< "$c"
+      env "${envs[@]}" timeout -k 10 600 python -u bench.py --config "$b" --no-cpu-baseline ${d//+/ } > "$O/var_$a.log" 2>&1 || { r=$?; tail -20 "$O/var_$a.log"; return $r; }
+      echo "  $a $(grep '^{' "$O/var_$a.log" | python3 -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('avg_launch_ms'), (d.get('roofline') or {}).get('frac'))")" ;;
     py)
       timeout -k 10 600 python -u "tools/$a" ${b//+/ } > "$O/${a%.py}.log" 2>&1 || { r=$?; tail -20 "$O/${a%.py}.log"; return $r; }
       tail -5 "$O/${a%.py}.log" ;;
