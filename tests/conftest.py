@@ -11,6 +11,21 @@ for p in (ROOT, os.path.join(ROOT, "mpistragglers.jl_amd"), os.path.join(ROOT, "
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "timing: checks host-time latencies against the oracle's clock; "
+                                       "runs after the other tests (pytest_collection_modifyitems)")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    """Order: every other test, then the timing checks (latency against the oracle's virtual
+    clock: a stall of the box inflates them, so they go where a miss under `-x` costs no other
+    test), then the multi-process GPU tests (test_gpu_procs.py; the single-process timing checks
+    right after them were disturbed).  The sort is stable: file and definition
+    order are kept inside each group."""
+    def group(item):
+        if item.fspath.basename == "test_gpu_procs.py":
+            return 2
+        return 1 if item.get_closest_marker("timing") else 0
+    items.sort(key=group)
 
 
 @pytest.fixture(scope="session")

@@ -135,6 +135,48 @@ def random_scenario(seed):
     return {"name": f"rand{seed}", "n": n, "worker": "kmap2", "durations_ns": d.ravel().tolist(), "ops": ops}
 
 
+def _watchdog_loop(conn):
+    """Sleep 0.5 ms at a time; on each request reply (worst oversleep in ms, how many > 2 ms)
+    since the previous request."""
+    worst, over = 0.0, 0
+    while True:
+        if conn.poll():
+            if conn.recv() is None:
+                return
+            conn.send((round(worst, 3), over))
+            worst, over = 0.0, 0
+        t0 = time.perf_counter()
+        time.sleep(0.0005)
+        d = (time.perf_counter() - t0 - 0.0005) * 1e3
+        worst = max(worst, d)
+        over += d > 2.0
+
+
+class HostWatchdog:
+    """A process beside the test (same cgroup, no GPU) that measures how late its own 0.5 ms
+    sleeps wake: a host-wide stall (CPU throttling, descheduling by other tenants of the
+    machine) shows there as well as in the pool's host-time latencies.  take() returns the
+    worst oversleep (ms) and the count over 2 ms since the previous take()."""
+
+    def __init__(self):
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")
+        self._conn, child = ctx.Pipe()
+        self._proc = ctx.Process(target=_watchdog_loop, args=(child,), daemon=True)
+        self._proc.start()
+
+    def take(self):
+        self._conn.send(1)
+        return self._conn.recv()
+
+    def close(self):
+        try:
+            self._conn.send(None)
+        except OSError:
+            pass
+        self._proc.join(5)
+
+
 def warm_kernels(M, torch, n):
     """Load the task / sleep / exchange code objects before a timing-sensitive trace (a
     first launch loads its code object)."""

@@ -49,6 +49,7 @@ def test_kmap1(M, torch_mod):
     assert isendbuf.cpu().tolist() == [3.14, 3.14]                 # kmap1.jl:30
 
 
+@pytest.mark.timing
 @pytest.mark.parametrize("nranks", [3, 10])
 def test_kmap2(M, torch_mod, nranks):
     """test/kmap2.jl end to end on device workers; delays = the reference's distribution / 10."""
@@ -141,6 +142,7 @@ def test_queue_cap(M, torch_mod):
     c.close()
 
 
+@pytest.mark.timing
 def test_delay_calibration(M, torch_mod):
     """An injected delay of d ms shows up as a latency of d ms (within 0.5 ms)."""
     torch = torch_mod

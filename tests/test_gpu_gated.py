@@ -42,6 +42,13 @@ def M(built):
     return mpiasyncpools
 
 
+@pytest.fixture(scope="module")
+def watchdog():
+    w = gated.HostWatchdog()
+    yield w
+    w.close()
+
+
 def _kmap2_run(M, sc, delays):
     import torch
     _, sched = gated.oracle_gate(sc)
@@ -79,24 +86,32 @@ def _latency_check(name, sc, got):
     return not bad and np.median(dev) < 0.2e-3, msg
 
 
+@pytest.mark.timing
 @pytest.mark.parametrize("name", [s["name"] for s in SCEN])
-def test_golden_scenario_gated_on_device(M, name):
+def test_golden_scenario_gated_on_device(M, watchdog, name):
     """Every golden scenario at its committed durations: the trace bit-exact; the latency
     (host time, dispatch -> harvest, src/MPIAsyncPools.jl:105,164,215) within 1 ms of the
     oracle's at every harvest, plus 50 us per task completion inside that harvest's window
     (gated.latency_tolerance: the physical timeline's per-task overhead), median < 0.2 ms.
     Round 3's 10-50 ms outliers were launches stalled on a process holding more HSA queues
-    than the GPU maps (profiles/r04_gated_stall.txt); the process now holds at most 12.  A
-    timing miss is run again once (one environmental 61-65 ms stall of the GPU box in ~20
-    kmap2_n9 replays, r04_gated_stall.txt); the trace must be bit-exact in every run."""
+    than the GPU maps (profiles/r04_gated_stall.txt); the process now holds at most 12.  The
+    boxes also stall whole processes for 5-65 ms now and then (one 61-65 ms stall in ~20
+    kmap2_n9 replays; a watchdog process beside the replays saw a 7.2 ms oversleep of its own,
+    r04_gated_stall.txt): every in-flight task's latency then moves by the stall.  So a
+    timing miss runs the scenario again, up to three runs (the trace must be bit-exact in
+    every one), and the failure message carries the watchdog's worst oversleep per run.  The
+    test is marked `timing` and runs after the rest of the GPU suite (tests/conftest.py)."""
     sc = next(s for s in SCEN if s["name"] == name)
     comm_n = sc.get("comm_workers", sc["n"])
     dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(comm_n, -1)
     msgs = []
-    for attempt in range(2):
+    watchdog.take()
+    for attempt in range(3):
         got = _kmap2_run(M, sc, dur)
         assert gated.mismatches(name, got, sc["results"]) == []
         ok, msg = _latency_check(name, sc, got)
+        worst, over = watchdog.take()
+        msg += "; host watchdog worst oversleep %.2f ms (%d over 2 ms)" % (worst, over)
         msgs.append(msg)
         print(msg)
         if ok:

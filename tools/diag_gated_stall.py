@@ -5,8 +5,14 @@ only the streams it needs, then after a 16-worker comm has grown the process-wid
 pool (more HSA queues alive), and prints per run: the process's KFD queue count (when
 /sys exposes it), the latency deviation from the oracle (median / max / count > 1 ms), the
 timer thread's worst lateness against a due time and its worst launch-call duration.
-Usage (GPU box): python tools/diag_gated_stall.py [reps]
+Usage (GPU box): python tools/diag_gated_stall.py [reps] [scenario ...]
+  --stream  run the replays under a non-blocking torch stream (the coordinator's copies and the
+            harness's tensor ops off the legacy NULL stream, which orders against every blocking
+            worker stream)
+A watchdog process (same cgroup) sleeps 0.5 ms at a time and reports its worst oversleep per run:
+a host-wide stall (CPU throttling, descheduling) shows there as well as in the latencies.
 """
+import multiprocessing as mp
 import os
 import sys
 import time
@@ -31,7 +37,29 @@ def kfd_queues():
         return -1
 
 
+def watchdog(conn):
+    """Sleep 0.5 ms at a time; on each request reply (worst oversleep ms, count > 2 ms) since the last."""
+    worst, over = 0.0, 0
+    while True:
+        if conn.poll():
+            if conn.recv() is None:
+                return
+            conn.send((worst, over))
+            worst, over = 0.0, 0
+        t0 = time.perf_counter()
+        time.sleep(0.0005)
+        d = (time.perf_counter() - t0 - 0.0005) * 1e3
+        worst = max(worst, d)
+        over += d > 2.0
+
+
+WD = None
+
+
 def run(sc):
+    if WD is not None:
+        WD.send(1)
+        WD.recv()
     _, sched = gated.oracle_gate(sc)
     n = sc["n"]
     dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(n, -1)
@@ -44,9 +72,19 @@ def run(sc):
     def buf(k):
         return torch.zeros(k, dtype=torch.float64, device="cuda")
     t0 = time.time()
-    got, pool = gated.replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), gated.make_golden().predicate,
-                             snap=lambda t: t.clone())
+    if STREAM:
+        with torch.cuda.stream(torch.cuda.Stream()):
+            got, pool = gated.replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), gated.make_golden().predicate,
+                                     snap=lambda t: t.clone())
+            torch.cuda.current_stream().synchronize()
+    else:
+        got, pool = gated.replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), gated.make_golden().predicate,
+                                 snap=lambda t: t.clone())
     wall = time.time() - t0
+    wd = (-1.0, -1)
+    if WD is not None:
+        WD.send(1)
+        wd = WD.recv()
     q = kfd_queues()
     c = {k: comm.counter(k) for k in ("sleeps", "timer_late", "queues", "shared_worker_streams")}
     comm.shutdown()
@@ -68,14 +106,26 @@ def run(sc):
         print("    op %d %s worker %d: oracle %.3f ms device %.3f ms" % (
             k, sc["ops"][k], i, sc["results"][k]["latency_ns"][i] / 1e6, 1e3 * got[k]["latency_s"][i]))
     print("  kfd_queues %d  mismatches %d  wall %.1f s  latency dev median %.3f ms max %.3f ms  >1ms %d  worst %s  %s"
-          % (q, len(bad), wall, 1e3 * np.median(dev), 1e3 * dev.max(), int((dev > 1e-3).sum()), big, c), flush=True)
+          "  watchdog worst oversleep %.2f ms, %d > 2 ms%s"
+          % (q, len(bad), wall, 1e3 * np.median(dev), 1e3 * dev.max(), int((dev > 1e-3).sum()), big, c, wd[0], wd[1],
+             "  [non-blocking stream]" if STREAM else ""), flush=True)
+
+
+STREAM = False
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    if len(sys.argv) > 2:  # named scenarios only, fresh process
+    global STREAM, WD
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    STREAM = "--stream" in sys.argv
+    parent, child = mp.Pipe()
+    proc = mp.get_context("spawn").Process(target=watchdog, args=(child,), daemon=True)
+    proc.start()
+    WD = parent
+    reps = int(args[0]) if args else 4
+    if len(args) > 1:  # named scenarios only, fresh process
         torch.zeros(1, device="cuda")
-        for name in sys.argv[2:]:
+        for name in args[1:]:
             sc = next(s for s in gated.scenarios() if s["name"] == name)
             print("== %s" % name, flush=True)
             for _ in range(reps):
