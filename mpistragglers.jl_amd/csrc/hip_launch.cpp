@@ -298,7 +298,9 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
     // worker's chain of tasks: the gated kmap2_n9 replay drifted 1.2-1.9 ms from the
     // oracle's latencies by its 100th call with 40 us per task (profiles/r04_gated_stall.txt).
     const int64_t sleep_ns = delay - delay_lead_ns_;
-    if (sleep_ns > 0 && delay_on_device_) {
+    // a device sleep holds the worker's stream: on a stream another worker shares (past the
+    // queue cap) it would delay that worker too, so those sleeps stay on the host timer
+    if (sleep_ns > 0 && delay_on_device_ && !stream_shared(s)) {
       HIPCHECK(launch_sleep((unsigned long long)(double(sleep_ns) * rt_hz_ / 1e9), s));
       n_sleeps_ += 1;
       go();

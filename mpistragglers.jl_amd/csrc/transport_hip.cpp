@@ -117,11 +117,13 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   // where a process serves one worker
   const char* arm = std::getenv("MPA_ARM");
   arm_mode_ = arm && *arm == '0' ? 0 : arm && *arm == '1' ? 1 : 2;
-  // how an armed task waits: one wave ahead of it (default) or every workgroup in-kernel
+  // injected straggler delays: the host timer (default) or a sleep kernel ahead of the task on
+  // an unshared worker stream (MPA_DELAY=device); the launch overhead taken out of each sleep
   const char* dl = std::getenv("MPA_DELAY");
   delay_on_device_ = dl && !std::strcmp(dl, "device");
   const char* lead = std::getenv("MPA_DELAY_LEAD_NS");
   if (lead) delay_lead_ns_ = std::atoll(lead);
+  // how an armed task waits: one wave ahead of it (default) or every workgroup in-kernel
   const char* aw = std::getenv("MPA_ARM_WAIT");
   arm_wave_ = !(aw && !std::strcmp(aw, "kernel"));
   const char* cb = measure_env("MPA_COORD_BATCH");

@@ -28,3 +28,24 @@ def pytest_collection_modifyitems(session, config, items):
             return 2
         return 1 if item.fspath.basename == "test_gpu_procs.py" else 0
     items.sort(key=group)
+
+
+@pytest.fixture(scope="session")
+def built():
+    """Build the oracle (gcc) and the HIP library (hipcc) once per session if missing."""
+    import subprocess
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_build", "liboracle.so")):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"])
+    if not os.path.exists(os.path.join(ROOT, "mpistragglers.jl_amd", "_build", "libmpiasyncpools.so")):
+        subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "mpistragglers.jl_amd")])
+    return True
+
+
+@pytest.fixture(autouse=True)
+def _release_comms(request):
+    """After a GPU test, collect the comms it left unclosed: their streams go back to the
+    process's capped queue set (MPA_MAX_QUEUES), or the next comm's workers would share them."""
+    yield
+    if request.node.get_closest_marker("gpu"):
+        import gc
+        gc.collect()

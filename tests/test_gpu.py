@@ -143,6 +143,29 @@ def test_queue_cap(M, torch_mod):
     c.close()
 
 
+def test_device_delays_only_on_unshared_streams(M, torch_mod, monkeypatch):
+    """MPA_DELAY=device (opt-in): a delayed task sleeps in a one-wave kernel ahead
+    of it on its worker's stream -- but only where that stream is the worker's own: past the
+    queue cap workers share streams, and a sleep there would hold the other worker's tasks,
+    so those delays stay on the host timer.  16 workers over 12 streams: one sleep kernel per
+    unshared worker, every reply correct."""
+    monkeypatch.setenv("MPA_DELAY", "device")
+    torch = torch_mod
+    c = M.DeviceComm(16)
+    for r in range(1, 17):
+        c.set_task(r, "kmap2")
+        c.set_delays(r, [200_000])
+    pool = M.MPIAsyncPool(16)
+    rb = torch.zeros(48, dtype=torch.float64, device="cuda")
+    M.asyncmap_(pool, torch.ones(1, dtype=torch.float64, device="cuda"), rb,
+                torch.zeros(16, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), c, nwait=16)
+    shared = c.counter("shared_worker_streams")  # the streams were in place before the launches
+    assert 0 < shared < 16 and c.counter("queues") <= 12
+    assert c.counter("sleeps") == 16 - shared, (c.counter("sleeps"), shared)
+    assert rb.cpu().numpy().reshape(16, 3)[:, 0].tolist() == list(range(1, 17))
+    c.close()
+
+
 @pytest.mark.timing
 def test_delay_calibration(M, torch_mod):
     """An injected delay of d ms shows up as a latency of d ms (within 0.5 ms)."""
