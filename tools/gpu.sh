@@ -77,8 +77,11 @@ run_step() {
     var)
       # var:NAME:CFG:VAR=VAL,VAR=VAL[:ARGS]  one bench under extra environment -> var_NAME.log
       local envs=()
+      if [[ "$c" != *=* ]]; then  # no environment given: var:NAME:CFG:ARGS
+        d=$c; c=
+      fi
       IFS=',' read -r -a envs <<< "$c"
-      env "${envs[@]}" timeout -k 10 600 python -u bench.py --config "$b" --no-cpu-baseline ${d//+/ } > "$O/var_$a.log" 2>&1 || { r=$?; tail -20 "$O/var_$a.log"; return $r; }
+      env ${envs[@]+"${envs[@]}"} timeout -k 10 600 python -u bench.py --config "$b" --no-cpu-baseline ${d//+/ } > "$O/var_$a.log" 2>&1 || { r=$?; tail -20 "$O/var_$a.log"; return $r; }
       echo "  $a $(grep '^{' "$O/var_$a.log" | python3 -c "import json,sys;d=json.load(sys.stdin);print(d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('avg_launch_ms'), (d.get('roofline') or {}).get('frac'))")" ;;
     py)
       timeout -k 10 600 python -u "tools/$a" ${b//+/ } > "$O/${a%.py}.log" 2>&1 || { r=$?; tail -20 "$O/${a%.py}.log"; return $r; }
