@@ -84,6 +84,7 @@ def replay(M, sc, comm, buf, host, predicate, snap=None):
             t_end = time.perf_counter_ns() + int(op["advance_ns"])
             while time.perf_counter_ns() < t_end:
                 pass
+        t0 = time.perf_counter()
         if op["op"] == "waitall":
             M.waitall_(pool, recv, irecv)
         else:
@@ -91,9 +92,10 @@ def replay(M, sc, comm, buf, host, predicate, snap=None):
             nw = op.get("nwait")
             nw = predicate(nw) if isinstance(nw, str) else nw
             M.asyncmap_(pool, send, recv, isend, irecv, comm, nwait=nw, epoch=op.get("epoch"), tag=0)
+        call_ms = (time.perf_counter() - t0) * 1e3
         out.append({"repochs": pool.repochs.tolist(), "sepochs": pool.sepochs.tolist(),
                     "active": pool.active.astype(int).tolist(), "epoch": int(pool.epoch),
-                    "latency_s": pool.latency.tolist(), "recv": snap(recv)})
+                    "latency_s": pool.latency.tolist(), "recv": snap(recv), "call_ms": call_ms})
     for r in out:
         r["recv"] = np.asarray(host(r["recv"])).tolist()
     return out, pool

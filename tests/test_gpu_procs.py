@@ -2,9 +2,7 @@
 processes on the same GPU) serve workers through the shared-memory mailboxes; kmap2.jl
 properties across processes and least-squares epochs checked against the fp64 oracle.
 
-(Named to run after the single-process GPU tests: in round 4 the gated replays' latencies
-were disturbed for about a minute after the eight-process tests had run and exited,
-profiles/r04_gated_stall.txt.)"""
+(They run after the other GPU tests and before the timing checks, tests/conftest.py.)"""
 import multiprocessing as mp
 import random
 
