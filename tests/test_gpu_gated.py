@@ -49,7 +49,22 @@ def watchdog():
     w.close()
 
 
-def _kmap2_run(M, sc, delays):
+def _kmap2_run(M, sc, delays, own_stream=False):
+    """One gated replay of a kmap2 scenario.  own_stream: the harness (its buffers, the send
+    writes, the recvbuf snapshots) and the coordinator's copies run on a stream of their own, a
+    non-blocking one, as a GPU caller of the pool would keep them: on the legacy NULL stream
+    every harness op between two calls also orders against every worker stream, so a worker
+    task the GPU starts late delays the next dispatch too (profiles/r04_gated_stall.txt)."""
+    import contextlib
+    import torch
+    ctx = torch.cuda.stream(torch.cuda.Stream()) if own_stream else contextlib.nullcontext()
+    with ctx:
+        got = _kmap2_replay(M, sc, delays)
+        torch.cuda.current_stream().synchronize()
+    return got
+
+
+def _kmap2_replay(M, sc, delays):
     import torch
     _, sched = gated.oracle_gate(sc)
     comm_n = sc.get("comm_workers", sc["n"])
@@ -113,7 +128,9 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
     the scenario again after a 10 s pause, up to five runs (the trace must be bit-exact in
     every one; each run is held to the full bound), and the failure message carries, per run,
     the watchdog's worst oversleep, the calls' durations at the missed harvests and the
-    transport's counters.  The test is marked `timing` and runs last (tests/conftest.py)."""
+    transport's counters.  The harness runs on a non-blocking stream of its own (_kmap2_run);
+    the NULL-stream caller is covered by the random scenarios and the config replays.  The
+    test is marked `timing` and runs last (tests/conftest.py)."""
     sc = next(s for s in SCEN if s["name"] == name)
     comm_n = sc.get("comm_workers", sc["n"])
     dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(comm_n, -1)
@@ -124,7 +141,7 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
         if attempt:
             time.sleep(10)  # a noisy spell of the box passes (r04flaky: three misses in a row, then clean)
             watchdog.take()
-        got = _kmap2_run(M, sc, dur)
+        got = _kmap2_run(M, sc, dur, own_stream=True)
         assert gated.mismatches(name, got, sc["results"]) == []
         ok, msg = _latency_check(name, sc, got)
         worst, over = watchdog.take()
