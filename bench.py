@@ -267,7 +267,7 @@ def report(args, cfg, world, el, per_rank, extra):
     per_launch_bytes = kbytes / max(kl, 1)
     per_launch_s = kms / 1e3 / max(kl, 1)
     # HBM traffic per launch: NOT measured in this run (PMC counters need their own
-    # rocprofv3 --pmc passes, tools/gpu_profile.sh); read from the committed summary of the
+    # rocprofv3 --pmc passes: tools/gpu.sh pmc, tools/pmc_summarize.py); read from the committed summary of the
     # same command and labelled with its file and date
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", f"lsq_pmc_{cfg['config']}.json")
