@@ -84,7 +84,7 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 }
 // MPA_LSQP4_PROBE (timing-probe builds only, wrong results: make BUILD=... EXTRA=-DMPA_LSQP4_PROBE=n,
 // profiles/r03_c5_probes.txt): 1 no strip DMAs in the block loop, 2 no cross-wave exchange /
-// barrier in the reduce, 4 no phase-1 MFMAs
+// barrier in the reduce, 4 no phase-1 MFMAs, 8 half the phase-2 LDS reads (r04_c5_pipelined.txt)
 #ifndef MPA_LSQP4_PROBE
 #define MPA_LSQP4_PROBE 0
 #endif
@@ -491,6 +491,13 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     auto rd = [&](int c, s16x4 (&d)[CH][2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
+#if MPA_LSQP4_PROBE & 8  // timing probe 8: half the phase-2 reads (odd tiles reuse the even tile's)
+        if (k & 1) {
+          d[k][0] = d[k - 1][0];
+          d[k][1] = d[k - 1][1];
+          continue;
+        }
+#endif
         const uint8_t* src = slot + off2[k] + 2048 * c;
         d[k][0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(src));
         d[k][1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(src + 4 * 128));
