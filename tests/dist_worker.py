@@ -13,6 +13,16 @@ for p in (ROOT, os.path.join(ROOT, "mpistragglers.jl_amd")):
         sys.path.insert(0, p)
 
 
+def free_port():
+    """A TCP port nothing listens on now (the kernel's pick for port 0): the rendezvous's.
+    A random pick from a fixed range collided with a socket a previous test had left in use
+    (EADDRINUSE, r04gc)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def _init(rank, world, port):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"

@@ -10,6 +10,8 @@ completions and the product must reproduce the oracle's trace bit for bit, whate
 the tasks really finish in (ties included: released together, Waitany! must take the
 lowest index, src/MPIAsyncPools.jl:161 over MPICH's array scan).
 """
+import contextlib
+import gc
 import importlib.util
 import json
 import os
@@ -63,6 +65,23 @@ def latency_tolerance(sc, slack_s=1e-3, per_event_s=50e-6):
             inside = int(np.searchsorted(done, seen, side="right") - np.searchsorted(done, post, side="right"))
             tol[(k, i)] = slack_s + per_event_s * max(inside - 1, 0)
     return tol
+
+
+@contextlib.contextmanager
+def no_gc():
+    """Python's cyclic garbage collector off for a timed stretch (collected once before): a
+    generation-2 pass over the heap of a long pytest process takes milliseconds to tens of
+    them and pauses the thread that dispatches and harvests, which the pool's host-time
+    latencies then record (r04final3: 5-46 ms misses with the host watchdog and the
+    transport's timer on time, profiles/r04_gated_stall.txt)."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def replay(M, sc, comm, buf, host, predicate, snap=None):

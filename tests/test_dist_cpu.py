@@ -4,7 +4,6 @@ mailboxes (MPA_TRANSPORT_HOST: the HIP transport's protocol with host-executed t
 workers).  Checks the test/kmap2.jl properties across processes, pause/resume between
 serve() sessions, waitall!, the predicate form of nwait, and shutdown."""
 import multiprocessing as mp
-import random
 
 import pytest
 
@@ -14,7 +13,7 @@ import dist_worker
 def _run(world, placement):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = random.randint(20000, 40000)
+    port = dist_worker.free_port()
     procs = [ctx.Process(target=dist_worker.kmap2_dist, args=(r, world, port, "host", placement, q))
              for r in range(world)]
     for p in procs:

@@ -95,12 +95,13 @@ def test_kmap2(M, torch_mod, nranks):
         if attempt:
             time.sleep(10)  # a noisy spell of the box passes (profiles/r04_gated_stall.txt)
         dev = []
-        for _ in range(100):
-            t0 = time.perf_counter()
-            repochs = M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=f, tag=0)
-            delay = time.perf_counter() - t0
-            assert repochs[0] == pool.epoch
-            dev.append(abs(delay - pool.latency[0]))
+        with gated_mod().no_gc():  # a GC pass inside the call's Python wrapper is call time, not latency
+            for _ in range(100):
+                t0 = time.perf_counter()
+                repochs = M.asyncmap_(pool, sendbuf, recvbuf, isendbuf, irecvbuf, comm, nwait=f, tag=0)
+                delay = time.perf_counter() - t0
+                assert repochs[0] == pool.epoch
+                dev.append(abs(delay - pool.latency[0]))
         dev = np.sort(np.asarray(dev))
         print("kmap2.jl:71 run %d: |call time - latency| max %.3f ms" % (attempt, 1e3 * dev[-1]))
         if dev[-1] <= 1e-3:
@@ -112,6 +113,11 @@ def test_kmap2(M, torch_mod, nranks):
     for i in range(nworkers):
         assert rb[i, 1] == comm.tasks_done(i + 1)
     comm.shutdown()
+
+
+def gated_mod():
+    import gated
+    return gated
 
 
 def _warm_kernels(M, torch, n):
@@ -185,11 +191,12 @@ def test_delay_calibration(M, torch_mod):
         if attempt:
             __import__("time").sleep(10)  # a noisy spell of the box passes
         lat = []
-        for _ in range(3):
-            M.asyncmap_(pool, s, torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"),
-                        comm, nwait=2)
-            # the delay is dispatch -> reply (the task's ~35 us launch overhead is inside it)
-            lat.append((float(pool.latency[0]), float(pool.latency[1])))
+        with gated_mod().no_gc():
+            for _ in range(3):
+                M.asyncmap_(pool, s, torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"),
+                            torch.zeros(4, device="cuda"), comm, nwait=2)
+                # the delay is dispatch -> reply (the task's ~35 us launch overhead is inside it)
+                lat.append((float(pool.latency[0]), float(pool.latency[1])))
         ok = all(abs(a - 0.020) < 0.5e-3 and abs(b - 0.007) < 0.5e-3 for a, b in lat)
         print("delay calibration run %d: %s" % (attempt, lat))
         if ok:

@@ -58,7 +58,7 @@ def _kmap2_run(M, sc, delays, own_stream=False):
     import contextlib
     import torch
     ctx = torch.cuda.stream(torch.cuda.Stream()) if own_stream else contextlib.nullcontext()
-    with ctx:
+    with ctx, gated.no_gc():
         got = _kmap2_replay(M, sc, delays)
         torch.cuda.current_stream().synchronize()
     return got

@@ -4,7 +4,6 @@ properties across processes and least-squares epochs checked against the fp64 or
 
 (They run after the other GPU tests and before the timing checks, tests/conftest.py.)"""
 import multiprocessing as mp
-import random
 
 import pytest
 
@@ -16,7 +15,7 @@ pytestmark = pytest.mark.gpu
 def _run(target, world, *args, timeout=180):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = random.randint(20000, 40000)
+    port = dist_worker.free_port()
     procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
     for p in procs:
         p.start()
