@@ -6,6 +6,7 @@ pool (more HSA queues alive), and prints per run: the process's KFD queue count 
 /sys exposes it), the latency deviation from the oracle (median / max / count > 1 ms), the
 timer thread's worst lateness against a due time and its worst launch-call duration.
 Usage (GPU box): python tools/diag_gated_stall.py [reps] [scenario ...]
+  --grow=N  (named scenarios) a N-worker comm fills the process's stream pool first
   --stream  run the replays under a non-blocking torch stream (the coordinator's copies and the
             harness's tensor ops off the legacy NULL stream, which orders against every blocking
             worker stream)
@@ -123,8 +124,14 @@ def main():
     proc.start()
     WD = parent
     reps = int(args[0]) if args else 4
-    if len(args) > 1:  # named scenarios only, fresh process
+    grow = next((int(a.split("=")[1]) for a in sys.argv[1:] if a.startswith("--grow=")), 0)
+    if len(args) > 1:  # named scenarios only, fresh process (--grow=N: a N-worker comm fills the pool first)
         torch.zeros(1, device="cuda")
+        if grow:
+            big = M.DeviceComm(grow)
+            for r in range(1, grow + 1):
+                big.set_task(r, "kmap2")
+            big.close()
         for name in args[1:]:
             sc = next(s for s in gated.scenarios() if s["name"] == name)
             print("== %s" % name, flush=True)
