@@ -135,6 +135,68 @@ def mismatches(name, got, ref):
     return bad
 
 
+def kmap2_replay(M, sc, delays, own_stream=False):
+    """One gated replay of a kmap2 scenario on device workers whose injected delays are
+    `delays` (workers x tasks, ns; None: none): (the oracle-layout record, the transport's
+    counters).  own_stream: the harness (its buffers, the send writes, the recvbuf snapshots)
+    and the coordinator's copies run on a non-blocking stream of their own, as a GPU caller
+    of the pool would keep them: on the legacy NULL stream every harness op between two calls
+    also orders against every worker stream.  The whole replay runs with Python's GC off."""
+    import torch
+    ctx = torch.cuda.stream(torch.cuda.Stream()) if own_stream else contextlib.nullcontext()
+    with ctx, no_gc():
+        _, sched = oracle_gate(sc)
+        comm_n = sc.get("comm_workers", sc["n"])
+        comm = M.DeviceComm(comm_n)
+        for r in range(1, comm_n + 1):
+            comm.set_task(r, "kmap2")
+            if delays is not None:
+                comm.set_delays(r, delays[r - 1])
+        comm.set_gate(*sched)
+
+        def buf(k):
+            return torch.zeros(k, dtype=torch.float64, device="cuda")
+        got, pool = replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), make_golden().predicate,
+                           snap=lambda t: t.clone())
+        counters = {k: comm.counter(k) for k in ("timer_late", "queues", "shared_worker_streams")}
+        comm.shutdown()
+        comm.close()
+        torch.cuda.current_stream().synchronize()
+    return got, counters
+
+
+def _child_replay(name, own_stream, q):
+    try:
+        import torch
+        import mpiasyncpools as M
+        torch.zeros(1, device="cuda")
+        warm_kernels(M, torch, 4)
+        sc = next(s for s in scenarios() if s["name"] == name)
+        comm_n = sc.get("comm_workers", sc["n"])
+        dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(comm_n, -1)
+        q.put(("ok",) + kmap2_replay(M, sc, dur, own_stream))
+    except BaseException as e:  # report, do not hang the parent
+        q.put(("error", repr(e), {}))
+
+
+def kmap2_replay_in_child(name, own_stream=True, timeout=300):
+    """kmap2_replay of the golden scenario `name` in a fresh (spawned) process."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_child_replay, args=(name, own_stream, q))
+    p.start()
+    try:
+        status, got, counters = q.get(timeout=timeout)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    if status != "ok":
+        raise RuntimeError("replay of %s in a child process failed: %s" % (name, got))
+    return got, dict(counters, fresh_process=1)
+
+
 def random_scenario(seed):
     """A random pool / schedule / op mix (ties from 0-5 ms durations, nwait integers,
     counting predicates and test/kmap2.jl:65's predicate, explicit epochs, waitall!s)."""

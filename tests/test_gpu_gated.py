@@ -50,43 +50,14 @@ def watchdog():
 
 
 def _kmap2_run(M, sc, delays, own_stream=False):
-    """One gated replay of a kmap2 scenario.  own_stream: the harness (its buffers, the send
-    writes, the recvbuf snapshots) and the coordinator's copies run on a stream of their own, a
-    non-blocking one, as a GPU caller of the pool would keep them: on the legacy NULL stream
-    every harness op between two calls also orders against every worker stream, so a worker
-    task the GPU starts late delays the next dispatch too (profiles/r04_gated_stall.txt)."""
-    import contextlib
-    import torch
-    ctx = torch.cuda.stream(torch.cuda.Stream()) if own_stream else contextlib.nullcontext()
-    with ctx, gated.no_gc():
-        got = _kmap2_replay(M, sc, delays)
-        torch.cuda.current_stream().synchronize()
-    return got
-
-
-def _kmap2_replay(M, sc, delays):
-    import torch
-    _, sched = gated.oracle_gate(sc)
-    comm_n = sc.get("comm_workers", sc["n"])
-    comm = M.DeviceComm(comm_n)
-    for r in range(1, comm_n + 1):
-        comm.set_task(r, "kmap2")
-        if delays is not None:
-            comm.set_delays(r, delays[r - 1])
-    comm.set_gate(*sched)
-
-    def buf(k):
-        return torch.zeros(k, dtype=torch.float64, device="cuda")
-    got, pool = gated.replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), gated.make_golden().predicate,
-                             snap=lambda t: t.clone())
+    """One gated replay of a kmap2 scenario in this process (gated.kmap2_replay)."""
+    got, counters = gated.kmap2_replay(M, sc, delays, own_stream)
     _LAST.clear()
-    _LAST.update({k: comm.counter(k) for k in ("timer_late", "queues", "shared_worker_streams")})
-    comm.shutdown()
-    comm.close()
+    _LAST.update(counters)
     return got
 
 
-_LAST = {}  # the transport's counters of the last _kmap2_run (failure messages)
+_LAST = {}  # the transport's counters of the last replay (failure messages)
 
 
 def _latency_check(name, sc, got):
@@ -128,7 +99,9 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
     the scenario again after a 10 s pause, up to five runs (the trace must be bit-exact in
     every one; each run is held to the full bound), and the failure message carries, per run,
     the watchdog's worst oversleep, the calls' durations at the missed harvests and the
-    transport's counters.  The harness runs on a non-blocking stream of its own (_kmap2_run);
+    transport's counters; runs 3-5 go to a fresh process (the misses showed in the long-lived
+    suite process, never in the standalone replays).  The harness runs on a non-blocking stream
+    of its own (gated.kmap2_replay);
     the NULL-stream caller is covered by the random scenarios and the config replays.  The
     test is marked `timing` and runs last (tests/conftest.py)."""
     sc = next(s for s in SCEN if s["name"] == name)
@@ -141,7 +114,12 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
         if attempt:
             time.sleep(10)  # a noisy spell of the box passes (r04flaky: three misses in a row, then clean)
             watchdog.take()
-        got = _kmap2_run(M, sc, dur, own_stream=True)
+        if attempt < 2:
+            got = _kmap2_run(M, sc, dur, own_stream=True)
+        else:  # in a fresh process: the misses came from the long-lived suite process (r04_gated_stall.txt)
+            got, counters = gated.kmap2_replay_in_child(name, own_stream=True)
+            _LAST.clear()
+            _LAST.update(counters)
         assert gated.mismatches(name, got, sc["results"]) == []
         ok, msg = _latency_check(name, sc, got)
         worst, over = watchdog.take()

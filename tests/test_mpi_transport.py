@@ -44,19 +44,35 @@ def test_mpi_library_exports_its_header(driver):
     assert b"MPI is not initialized" in main.mpa_last_error()
 
 
+def _mpi_trace_mismatches(sc, out):
+    lines = [ln for ln in out.stdout.splitlines() if "|" in ln]
+    if out.returncode != 0 or len(lines) != len(sc["results"]):
+        return ["rc %d, %d of %d lines: %s" % (out.returncode, len(lines), len(sc["results"]), out.stderr[-2000:])]
+    bad = []
+    for k, (ln, ref) in enumerate(zip(lines, sc["results"])):
+        rep, act, rec = ln.split("|")
+        if ([int(v) for v in rep.split()] != ref["repochs"] or [int(v) for v in act.split()] != ref["active"]
+                or [float(v) for v in rec.split()] != ref["recv"]):
+            bad.append((k, ln))
+    return bad
+
+
 @pytest.mark.parametrize("name", SEPARATED)
 def test_pool_over_mpi_matches_golden_trace(driver, tmp_path, name):
+    """The pool over MPICH with worker processes sleeping the schedule's durations (x4): the
+    oracle's trace.  The schedules' completions are >= 4 ms apart (x4: 16 ms), but this
+    container's 8 CPUs also run the rest of the suite, and a worker process scheduled late
+    can reorder two completions; a divergent run is repeated once at x8 (as the MPICH replay
+    test does), and the second run's trace must be the oracle's."""
     sc = next(s for s in GOLD if s["name"] == name)
     f = tmp_path / "scenario.txt"
     f.write_text(scenario_text(sc))
     env = dict(os.environ, HYDRA_LAUNCHER="fork")
-    out = subprocess.run([MPIEXEC, "-n", str(sc["n"] + 1), driver, str(f), "4"], capture_output=True, text=True,
-                         timeout=120, env=env)
-    assert out.returncode == 0, out.stderr[-2000:]
-    lines = [ln for ln in out.stdout.splitlines() if "|" in ln]
-    assert len(lines) == len(sc["results"])
-    for k, (ln, ref) in enumerate(zip(lines, sc["results"])):
-        rep, act, rec = ln.split("|")
-        assert [int(v) for v in rep.split()] == ref["repochs"], (name, k, ln)
-        assert [int(v) for v in act.split()] == ref["active"], (name, k, ln)
-        assert [float(v) for v in rec.split()] == ref["recv"], (name, k, ln)
+    for scale in ("4", "8"):
+        out = subprocess.run([MPIEXEC, "-n", str(sc["n"] + 1), driver, str(f), scale], capture_output=True,
+                             text=True, timeout=240, env=env)
+        bad = _mpi_trace_mismatches(sc, out)
+        if not bad:
+            break
+        print("%s at x%s: %d divergent calls, first %s" % (name, scale, len(bad), bad[:1]))
+    assert bad == [], (name, bad[:3])
