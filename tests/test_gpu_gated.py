@@ -76,9 +76,10 @@ def _latency_check(name, sc, got):
         name, 1e3 * np.median(dev), 1e3 * dev.max(), bad[:6])
     if bad:  # what the calls around the misses took, and the transport's view
         ops = sorted({k for k, _, _, _ in bad})[:6]
-        msg += "; call ms at those ops %s; counters %s; loadavg %s" % (
+        import os
+        msg += "; call ms at those ops %s; counters %s; loadavg %s; this process's threads %d" % (
             [(k, round(got[k].get("call_ms", -1.0), 2)) for k in ops], dict(_LAST),
-            tuple(round(x, 1) for x in __import__("os").getloadavg()))
+            tuple(round(x, 1) for x in os.getloadavg()), len(os.listdir("/proc/self/task")))
     return not bad and np.median(dev) < 0.2e-3, msg
 
 
