@@ -97,8 +97,10 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
     r04_gated_stall.txt): every in-flight task's latency then moves by the stall; and some
     boxes go through noisy spells of 1-20 ms misses that neither the host watchdog nor the
     timer sees (GPU side; r04flaky: three runs in a row, then clean).  So a timing miss runs
-    the scenario again after a 10 s pause, up to five runs (the trace must be bit-exact in
-    every one; each run is held to the full bound), and the failure message carries, per run,
+    the scenario again after a 10 s pause -- up to five misses on a quiet host, eight runs in
+    all (a miss during which the watchdog itself overslept past 2 ms is the box's; the trace
+    must be bit-exact in every run; each run is held to the full bound) -- and the failure
+    message carries, per run,
     the watchdog's worst oversleep, the calls' durations at the missed harvests and the
     transport's counters; runs 3-5 go to a fresh process (the misses showed in the long-lived
     suite process, never in the standalone replays).  The harness runs on a non-blocking stream
@@ -111,7 +113,8 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
     import time
     msgs = []
     watchdog.take()
-    for attempt in range(5):
+    quiet_misses = 0
+    for attempt in range(8):
         if attempt:
             time.sleep(10)  # a noisy spell of the box passes (r04flaky: three misses in a row, then clean)
             watchdog.take()
@@ -128,6 +131,11 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
         msgs.append(msg)
         print(msg)
         if ok:
+            break
+        # a miss while the host itself stalled (the watchdog overslept past 2 ms) is the box's; five
+        # misses on a quiet host are the product's
+        quiet_misses += over == 0
+        if quiet_misses == 5:
             break
     assert ok, msgs
 
