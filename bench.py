@@ -241,13 +241,17 @@ def exchange_report(xt):
 
 def timing_period(args, cfg):
     """HIP events on one launch in k: the config's k, lowered so that a short run still times
-    at least 16 launches (a 20-step c2 line at 1 in 8 timed only 3)."""
+    at least 16 launches (a 20-step c2 line at 1 in 8 timed only 3), but
+    never below 2 on a k-of-n config (c1): with every launch timed the transport pre-arms none
+    (transport_hip.cpp maybe_prearm), so a short line would measure another path than the
+    shipped one.  nwait = n configs (c2) never pre-arm: every launch may be timed."""
     if getattr(args, "timing_period", None):
         return args.timing_period
     k = cfg.get("timing_period", 1)
     steps = getattr(args, "steps", None)
     if steps:
-        k = max(1, min(k, steps // 16))
+        floor = 2 if k > 1 and cfg["nwait"] != cfg["workers"] else 1
+        k = max(floor, min(k, steps // 16))
     return k
 
 

@@ -22,10 +22,14 @@ int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares la
 // and torch's own); a comm returns its streams here, the next one reuses them, and past the
 // cap workers share the least-used stream (a delayed worker then sleeps on a shared queue:
 // stream_shared()).
+// Past the cap a stream is only shared with streams of its own kind: a launch stream never
+// carries a worker's (possibly sleeping, delayed) tasks, so a batch never queues behind an
+// unrelated straggler.
 struct QueueStream {
   int device;
   hipStream_t s;
   int users;
+  bool launch;
 };
 std::mutex g_stream_mu;
 std::vector<QueueStream> g_streams;
@@ -49,7 +53,7 @@ void destroy_pooled_streams() {
   g_streams.clear();
 }
 
-hipStream_t make_queue_stream(int device) {
+hipStream_t make_queue_stream(int device, bool launch) {
   static const bool registered = (std::atexit(destroy_pooled_streams), true);
   (void)registered;
   std::lock_guard<std::mutex> lk(g_stream_mu);
@@ -58,16 +62,19 @@ hipStream_t make_queue_stream(int device) {
     if (q.device == device) {
       if (q.users == 0) {
         q.users = 1;
+        q.launch = launch;
         return q.s;
       }
       ++have;
     }
-  if (have >= queue_cap()) {  // share the least-used one
+  if (have >= queue_cap()) {  // share the least-used one of the same kind
     QueueStream* best = nullptr;
     for (auto& q : g_streams)
-      if (q.device == device && (!best || q.users < best->users)) best = &q;
-    best->users += 1;
-    return best->s;
+      if (q.device == device && q.launch == launch && (!best || q.users < best->users)) best = &q;
+    if (best) {
+      best->users += 1;
+      return best->s;
+    }  // none of this kind yet: one more queue past the cap
   }
   hipDeviceProp_t p;
   HIPCHECK(hipGetDeviceProperties(&p, device));
@@ -76,15 +83,18 @@ hipStream_t make_queue_stream(int device) {
   if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
   hipStream_t s = nullptr;
   HIPCHECK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
-  g_streams.push_back({device, s, 1});
+  g_streams.push_back({device, s, 1, launch});
   return s;
 }
 
+// The comm's own work is drained by its teardown (hipDeviceSynchronize in ~HipComm); a stream
+// another live comm still uses is not synchronised here, so releasing never blocks on that
+// comm's work.
 void release_queue_stream(int device, hipStream_t s) {
-  (void)hipStreamSynchronize(s);
   std::lock_guard<std::mutex> lk(g_stream_mu);
   for (auto& q : g_streams)
     if (q.device == device && q.s == s && q.users > 0) {
+      if (q.users == 1) (void)hipStreamSynchronize(s);
       q.users -= 1;
       return;
     }
@@ -317,10 +327,12 @@ void HipComm::defer(uint64_t due, std::function<void()> go) {
   std::lock_guard<std::mutex> lk(tmu_);
   if (!timer_.joinable()) {
     tstop_ = false;
+    tstop_spin_.store(false, std::memory_order_release);
     timer_ = std::thread([this]() { timer_loop(); });
   }
   deferred_.push_back(Deferred{due, std::move(go)});
   std::push_heap(deferred_.begin(), deferred_.end());
+  tfront_.store(deferred_.front().due, std::memory_order_release);
   tcv_.notify_all();
 }
 
@@ -342,14 +354,19 @@ void HipComm::timer_loop() {
       continue;
     }
     if (now < due) {
+      // spin with the lock released; a task deferred meanwhile with an earlier deadline moves
+      // tfront_ below `due` and ends the spin (the loop then takes the new front), as does a stop
       lk.unlock();
-      while (mono_ns() < due) __builtin_ia32_pause();
+      while (mono_ns() < due && tfront_.load(std::memory_order_acquire) >= due &&
+             !tstop_spin_.load(std::memory_order_acquire))
+        __builtin_ia32_pause();
       lk.lock();
       continue;
     }
     std::pop_heap(deferred_.begin(), deferred_.end());
     Deferred d = std::move(deferred_.back());
     deferred_.pop_back();
+    tfront_.store(deferred_.empty() ? ~0ull : deferred_.front().due, std::memory_order_release);
     tbusy_ = true;
     lk.unlock();
     const uint64_t t_go = mono_ns();
@@ -370,7 +387,9 @@ void HipComm::stop_timer() {
   {
     std::lock_guard<std::mutex> lk(tmu_);
     tstop_ = true;
+    tstop_spin_.store(true, std::memory_order_release);
     deferred_.clear();
+    tfront_.store(~0ull, std::memory_order_release);
     tcv_.notify_all();
     tidle_.notify_all();
   }

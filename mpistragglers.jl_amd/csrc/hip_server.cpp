@@ -135,7 +135,7 @@ void HipComm::arm(int64_t rank) {
   w.out = reply_dst(w);
   hipStream_t st = worker_stream(w);
   unsigned long long* door = arm_wave_ ? nullptr : own_door(w);
-  if (arm_wave_) HIPCHECK(launch_door_wait(own_door(w), s, spin_ticks(), err_dev_, st));
+  if (arm_wave_) HIPCHECK(launch_door_wait(own_door(w), s, spin_ticks(), err_dev_, w.cancel_dev, st));
   double bytes = 0;
   if (ts.kind == MPA_TASK_LSQ) {
     LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes, armed_share());

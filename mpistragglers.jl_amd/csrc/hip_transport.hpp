@@ -86,7 +86,7 @@ inline int lsqb_grid(int pass) {
 // ~10 ms), so a destroyed comm returns its streams and the next comm reuses them; past the
 // cap (MPA_MAX_QUEUES) streams are shared.
 constexpr int kDefaultMaxQueues = 12;
-hipStream_t make_queue_stream(int device);
+hipStream_t make_queue_stream(int device, bool launch);
 void release_queue_stream(int device, hipStream_t s);
 bool stream_shared(hipStream_t s);  // more than one worker / comm launches on it
 int queue_streams(int device);      // CU-masked streams the process holds on the device
@@ -522,12 +522,12 @@ class HipComm final : public Comm {
 
   // the worker's own stream (delayed tasks, pre-armed tasks), created on first use
   hipStream_t worker_stream(HipWorker& w) {
-    if (!w.stream) w.stream = make_queue_stream(dev_);
+    if (!w.stream) w.stream = make_queue_stream(dev_, /*launch=*/false);
     return w.stream;
   }
   // launch stream k (created on first use, up to kLaunchStreams)
   hipStream_t launch_stream(size_t k) {
-    while (launch_streams_.size() <= k) launch_streams_.push_back(make_queue_stream(dev_));
+    while (launch_streams_.size() <= k) launch_streams_.push_back(make_queue_stream(dev_, /*launch=*/true));
     return launch_streams_[k];
   }
 
@@ -824,6 +824,11 @@ class HipComm final : public Comm {
   std::condition_variable tcv_, tidle_;
   std::vector<Deferred> deferred_;
   bool tstop_ = false, tbusy_ = false;
+  // the heap front's due time (~0: none) and a stop request, readable without tmu_: the timer's
+  // final spin watches them, so an earlier deadline deferred during the spin, or stop_timer,
+  // ends the spin at once
+  std::atomic<uint64_t> tfront_{~0ull};
+  std::atomic<bool> tstop_spin_{false};
   std::atomic<bool> tfailed_{false};
   std::mutex tfail_mu_;
   std::string tfail_msg_;

@@ -260,14 +260,20 @@ hipError_t launch_door_cas(unsigned long long* door, unsigned long long expect, 
 // moves on.  A waiting armed task holds one wave instead of its whole launch grid, so armed
 // worker processes sharing a GPU with rank 0 (a one-GPU rehearsal) cannot starve the
 // kernels that ring their doorbells (profiles/r03_rehearsal_n248.txt).
+// A wait that times out cancels the task queued behind it: the wave stores the
+// task's seq into the task's go word before it sets err bit 64, so the task -- the non-armed
+// instantiation, which only checks that word -- neither writes its reply nor publishes `done`
+// on a message rank 0 never posted.
 __global__ void __launch_bounds__(64) door_wait_kernel(const unsigned long long* door, unsigned long long seq,
-                                                       unsigned long long spin_ticks, unsigned* err) {
+                                                       unsigned long long spin_ticks, unsigned* err,
+                                                       unsigned long long* cancel) {
   if (threadIdx.x) return;
   const unsigned long long t0 = rt_now();
   for (unsigned k = 0; (__hip_atomic_load(door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & ~kCancelBit) < seq; ++k) {
     __builtin_amdgcn_s_sleep(2);
     if ((k & 255) == 255 && rt_now() - t0 > spin_ticks) {
-      __hip_atomic_fetch_or(err, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(cancel, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_fetch_or(err, 64u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
   }
@@ -275,8 +281,9 @@ __global__ void __launch_bounds__(64) door_wait_kernel(const unsigned long long*
 }
 
 hipError_t launch_door_wait(const unsigned long long* door, unsigned long long seq, unsigned long long spin_ticks,
-                            unsigned* err, hipStream_t s) {
-  hipLaunchKernelGGL(door_wait_kernel, dim3(1), dim3(64), 0, s, door, seq, spin_ticks, err);
+                            unsigned* err, unsigned long long* cancel, hipStream_t s) {
+  if (!door || !err || !cancel) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(door_wait_kernel, dim3(1), dim3(64), 0, s, door, seq, spin_ticks, err, cancel);
   return hipGetLastError();
 }
 

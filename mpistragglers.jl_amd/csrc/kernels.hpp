@@ -362,9 +362,10 @@ struct KmapArgs {
 };
 hipError_t launch_kmap(const KmapArgs& a, hipStream_t s);
 // one wave that waits for a device-armed task's doorbell (seq, with or without kCancelBit;
-// bounded by spin_ticks: err bit 64), then acquires at system scope; the task runs behind it
+// bounded by spin_ticks: on timeout it stores seq into `cancel`, the queued task's go word, so
+// the task cancels itself, and sets err bit 64), then acquires at system scope; the task runs behind it
 hipError_t launch_door_wait(const unsigned long long* door, unsigned long long seq, unsigned long long spin_ticks,
-                            unsigned* err, hipStream_t s);
+                            unsigned* err, unsigned long long* cancel, hipStream_t s);
 // one wave that spins `ticks` of s_memrealtime (a delayed worker's sleep, on its stream)
 hipError_t launch_sleep(unsigned long long ticks, hipStream_t s);
 // a worker process moves its device doorbell word (a device-armed task's cancel / restore,

@@ -59,6 +59,8 @@ def test_c1_samples_its_timing_events():
     a = _args()
     a.timing_period = 1
     assert bench.timing_period(a, cfg) == 1 and bench.timing_period(_args(steps=300), _cfg("c2")) == 8
+    # a short c1 line still leaves every other launch pre-armable: never below 2
+    assert bench.timing_period(_args(steps=20), cfg) == 2 and bench.timing_period(_args(steps=100), cfg) == 6
 
 
 def test_multi_gpu_rate_is_per_gpu_average_and_no_traffic():
