@@ -241,6 +241,19 @@ int mpa_comm_timing(mpa_comm* comm, double out[4]);
  * their inboxes)} since the previous call.  The broadcast of the iterate
  * (src/MPIAsyncPools.jl:130-138's Isend to every idle worker) is this kernel's remote part. */
 int mpa_comm_exchange_timing(mpa_comm* comm, double out[3]);
+/* HIP transport, diagnostics: the task trace.  mpa_comm_set_trace(comm, capacity) starts a
+ * trace of the next `capacity` posted tasks (0: off; the previous trace is dropped).
+ * mpa_comm_trace copies min(count recorded, capacity) entries of 10 int64 each into `out`:
+ * {rank, seq, post, due, call, ret, start, pub, seen, harvest}, host steady-clock ns, 0 where
+ * the task did not reach that point: post = dispatch (src/MPIAsyncPools.jl:130-137), due =
+ * post + its injected delay (the reference worker's reply time), call / ret = the launch call
+ * of its kernel entered / returned (the timer thread's for a delayed task), start / pub = the
+ * kernel's first instruction and its completion store on the device clock (s_memrealtime,
+ * mapped to host time by clock calibrations; the reference's worker programs only), seen = a
+ * gated replay observed the completion, harvest = phase 1 or the wait loop took it
+ * (:99-104, :161-167).  A late harvest splits into launch call, queue, kernel, visibility. */
+int mpa_comm_set_trace(mpa_comm* comm, int64_t capacity);
+int mpa_comm_trace(mpa_comm* comm, int64_t* out, int64_t capacity, int64_t* count);
 /* SIM transport only: compute time per task and the virtual clock */
 int mpa_comm_sim_set_compute(mpa_comm* comm, int64_t compute_ns);
 int mpa_comm_sim_advance(mpa_comm* comm, int64_t dt_ns);

@@ -6,11 +6,11 @@ own MPI verbs (Isend + Irecv!, Test!, Waitany!, Waitall!; src/MPIAsyncPools.jl:9
 are host arrays.  (UNEXECUTED here, see the module docstring; the C equivalent of this root
 side, tests/mpi/pool_mpi_kmap.c, runs the golden kmap2 scenarios over MPICH in the tests.)
 """
-module MPIAsyncPoolsHIPMPIExt
+module MPIAsyncPoolsMPIExt
 
 using MPI
-using MPIAsyncPoolsHIP
-using MPIAsyncPoolsHIP: AbstractComm, MPIAsyncPool, check, mpa_comm_destroy
+using MPIAsyncPools
+using MPIAsyncPools: AbstractComm, MPIAsyncPool, check, mpa_comm_destroy
 
 const libmpi_t = get(ENV, "MPA_MPI_LIB",
                      joinpath(@__DIR__, "..", "..", "..", "mpistragglers.jl_amd", "_build", "libmpiasyncpools_mpi.so"))

@@ -1,5 +1,5 @@
 """
-    MPIAsyncPoolsHIP
+    MPIAsyncPools
 
 The MI355X-native `asyncmap!` hot path behind the API of MPIAsyncPools.jl
 (severinson/MPIStragglers.jl, `src/MPIAsyncPools.jl`): `MPIAsyncPool(n)`,
@@ -14,7 +14,7 @@ so `repochs` returned by `asyncmap!` is the same vector later calls mutate
   * a `DistComm`: one process per GPU, as `mpiexec -n N julia ...` ranks (configs[2]-[4] on
     8 GPUs): every rank constructs it with the same placement, rank 0 calls `asyncmap!`,
     the others `serve!` their workers (examples/iterative_example.jl:84-88's rank split);
-  * or, with MPI.jl loaded (package extension `MPIAsyncPoolsHIPMPIExt`), a real `MPI.Comm`
+  * or, with MPI.jl loaded (package extension `MPIAsyncPoolsMPIExt`), a real `MPI.Comm`
     whose ranks run arbitrary worker programs (test/kmap1.jl, test/kmap2.jl unchanged).
 
 UNEXECUTED: Julia is not installed in the build image.  This module is written against the
@@ -24,7 +24,7 @@ arity); the Python binding drives the same ABI in every test, and a C client of 
 (`tests/c/capi_client.c`) runs it with exact-size device buffers on the GPU.  Its own
 behaviour (argument checks, conversions) is parity unpinned.
 """
-module MPIAsyncPoolsHIP
+module MPIAsyncPools
 
 export MPIAsyncPool, waitall!, DeviceComm, DistComm, set_task_lsq!, set_task_lsq_batch!, set_task_kmap!,
        set_delays!, shutdown!, serve!, pause_servers!, payload_path, lsq_descent!, lsqb_descent!, first_plus

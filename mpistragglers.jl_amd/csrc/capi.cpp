@@ -24,6 +24,8 @@ void* hip_get_stream(Comm* c);
 void hip_set_timing(Comm* c, int period);
 void hip_timing(Comm* c, double out[4]);
 void hip_exchange_timing(Comm* c, double out[3]);
+void hip_set_trace(Comm* c, int64_t capacity);
+int64_t hip_read_trace(Comm* c, int64_t* out, int64_t capacity);
 extern int g_lsq_grid;
 Comm* make_dist_comm(int64_t nworkers, const int* placement, int my_rank, const char* shm_name, size_t max_msg);
 void hip_serve(Comm* c);
@@ -345,6 +347,23 @@ int mpa_comm_exchange_timing(mpa_comm* comm, double out[3]) {
     need_hip(c);
     if (!out) mpa::fail(MPA_ARGUMENT_ERROR, "out is NULL");
     mpa::hip_exchange_timing(&c, out);
+  });
+}
+
+int mpa_comm_set_trace(mpa_comm* comm, int64_t capacity) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    mpa::hip_set_trace(&c, capacity);
+  });
+}
+
+int mpa_comm_trace(mpa_comm* comm, int64_t* out, int64_t capacity, int64_t* count) {
+  return guarded([&] {
+    mpa::Comm& c = comm_of(comm);
+    need_hip(c);
+    if (!count || capacity < 0 || (capacity > 0 && !out)) mpa::fail(MPA_ARGUMENT_ERROR, "bad trace buffer");
+    *count = mpa::hip_read_trace(&c, out, capacity);
   });
 }
 

@@ -74,6 +74,7 @@ void Comm::gate(int kind) {
         gate_poll(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
       std::this_thread::yield();
     }
+    gate_seen(r, gate_rel_[size_t(r - 1)]);
   }
   ++gate_step_;
 }

@@ -300,8 +300,15 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
       a.out = w.out;
       a.rl = w.rl;
       a.pub = Publish{w.flag_dev, err_dev_, w.seq, spin_ticks()};
-      go = [a, s]() { HIPCHECK(launch_kmap(a, s)); };
+      int64_t* e = trace_entry(w);
+      a.stamp = e ? reinterpret_cast<unsigned long long*>(e + kTStart) : nullptr;
+      go = [a, s, e]() {
+        if (e) e[kTCall] = int64_t(mono_ns());
+        HIPCHECK(launch_kmap(a, s));
+        if (e) e[kTRet] = int64_t(mono_ns());
+      };
     }
+    if (int64_t* e = trace_entry(w)) e[kTDue] = e[kTPost] + delay;
     // The oracle's worker replies exactly `delay` after its post; a launched task takes
     // ~30-40 us more (launch, the kernel, the completion word crossing the bus).  That
     // overhead is taken out of the sleep (delay_lead_ns_), or it would accumulate along every

@@ -147,6 +147,7 @@ struct HipWorker {
   // coordinator, launch-ahead: the next post / harvest of this worker is already enqueued
   bool preposted = false, preharvest = false;
   uint32_t arm_sbase = 0, arm_tbase = 0, arm_fsbase = 0, arm_ftbase = 0;
+  int64_t tslot = -1;  // task trace (mpa_comm_set_trace): the current task's entry, -1 none
 };
 
 // Accumulates copy items and doorbells into as few exchange launches as fit the kernel
@@ -642,6 +643,32 @@ class HipComm final : public Comm {
 
  public:
   void exchange_timing(double out[3]);
+
+  // ---- task trace (diagnostics; mpa_comm_set_trace / mpa_comm_trace) ----
+  // One entry per posted task of this process's workers, kTraceFields int64 each, host
+  // steady-clock ns (0: not reached): rank, seq, post (dispatch), due (post + injected delay,
+  // the oracle's completion time), call / ret (the launch call of the task kernel: entered,
+  // returned -- the timer thread's for a delayed task), start / pub (the kernel's first
+  // instruction and its completion store, read on the device's s_memrealtime and mapped to
+  // host time by two clock calibrations), seen (the gate observed the completion), harvest
+  // (phase 1 / wait loop took it).  Stamps are written for the reference's worker programs
+  // (kmap tasks); least-squares tasks get the host fields only.
+  static constexpr int kTraceFields = 10;
+  enum TraceField { kTRank, kTSeq, kTPost, kTDue, kTCall, kTRet, kTStart, kTPub, kTSeen, kTHarvest };
+  void set_trace(int64_t capacity);
+  int64_t read_trace(int64_t* out, int64_t capacity);
+  void gate_seen(int64_t rank, uint64_t seq) override;
+
+ private:
+  int64_t* trace_ = nullptr;  // host-pinned, capacity x kTraceFields
+  int64_t trace_cap_ = 0, trace_n_ = 0;
+  uint64_t* clock_probe_ = nullptr;  // host-pinned word the calibration kernel stores into
+  int64_t cal_ticks0_ = 0, cal_ns0_ = 0;  // (device ticks, host ns) at set_trace
+  void calibrate(int64_t* ticks, int64_t* ns);
+  void trace_post(HipWorker& w, int64_t rank);
+  int64_t* trace_entry(const HipWorker& w) {
+    return trace_ && w.tslot >= 0 ? trace_ + w.tslot * kTraceFields : nullptr;
+  }
 
  private:
   struct TimedLaunch {

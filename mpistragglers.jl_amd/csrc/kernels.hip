@@ -93,6 +93,7 @@ __global__ void __launch_bounds__(64) wait_words_kernel(WaitWordsArgs a) {
 
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) kmap_task_kernel(KmapArgs a) {
+  if (a.stamp && threadIdx.x == 0) __hip_atomic_store(a.stamp, rt_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (a.kind == MPA_TASK_ECHO) {
     const uint64_t m = a.sl < a.rl ? a.sl : a.rl;
     for (uint64_t j = threadIdx.x; j < a.rl; j += blockDim.x) a.out[j] = j < m ? a.x[j] : uint8_t(0);
@@ -107,7 +108,12 @@ __global__ void __launch_bounds__(64) kmap_task_kernel(KmapArgs a) {
   }
   drain_vm();
   __syncthreads();
+  if (a.stamp && threadIdx.x == 0) __hip_atomic_store(a.stamp + 1, rt_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (threadIdx.x == 0) publish_done(a.pub.flag, a.pub.seq);
+}
+
+__global__ void __launch_bounds__(64) clock_probe_kernel(unsigned long long* out) {
+  if (threadIdx.x == 0) __hip_atomic_store(out, rt_now(), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -302,6 +308,11 @@ __global__ void __launch_bounds__(64) sleep_kernel(unsigned long long ticks) {
 
 hipError_t launch_sleep(unsigned long long ticks, hipStream_t s) {
   hipLaunchKernelGGL(sleep_kernel, dim3(1), dim3(64), 0, s, ticks);
+  return hipGetLastError();
+}
+
+hipError_t launch_clock_probe(unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, s, out);
   return hipGetLastError();
 }
 

@@ -359,7 +359,12 @@ struct KmapArgs {
   uint8_t* out;
   uint64_t rl;
   Publish pub;
+  // task trace (host-pinned, may be null): [0] s_memrealtime at the kernel's start, [1] just
+  // before its completion store
+  unsigned long long* stamp;
 };
+// one wave stores s_memrealtime into *out (host-pinned): the task trace's clock calibration
+hipError_t launch_clock_probe(unsigned long long* out, hipStream_t s);
 hipError_t launch_kmap(const KmapArgs& a, hipStream_t s);
 // one wave that waits for a device-armed task's doorbell (seq, with or without kCancelBit;
 // bounded by spin_ticks: on timeout it stores seq into `cancel`, the queued task's go word, so

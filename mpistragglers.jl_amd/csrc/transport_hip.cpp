@@ -196,6 +196,8 @@ HipComm::~HipComm() {
   if (flags_) (void)hipHostFree(flags_);
   if (err_) (void)hipHostFree(err_);
   if (cancel_) (void)hipHostFree(cancel_);
+  if (trace_) (void)hipHostFree(trace_);
+  if (clock_probe_) (void)hipHostFree(clock_probe_);
   if (pre_mb_) {
     cancel_pre();
     (void)hipStreamSynchronize(coord_);  // the cancelled launch has left before its mailbox goes
@@ -235,6 +237,7 @@ void HipComm::post(int64_t i, int64_t rank, int64_t tag) {
            (long long)rank);
     w.preposted = false;
     w.seq += 1;
+    trace_post(w, rank);
     return;
   }
   if (w.remote) {
@@ -253,11 +256,13 @@ void HipComm::post(int64_t i, int64_t rank, int64_t tag) {
   w.sl = b_.sl;
   w.rl = b_.rl;
   w.seq += 1;
+  trace_post(w, rank);
   posts_.push_back(rank);
 }
 
 void HipComm::harvest(int64_t i, int64_t rank) {
   HipWorker& w = w_[size_t(rank - 1)];
+  if (int64_t* e = trace_entry(w)) e[kTHarvest] = int64_t(mono_ns());
   if (w.preharvest) {  // already in the epoch kernel enqueued ahead
     w.preharvest = false;
     return;
@@ -866,6 +871,86 @@ void* hip_get_stream(Comm* c) { return static_cast<HipComm*>(c)->stream(); }
 void hip_set_timing(Comm* c, int period) { static_cast<HipComm*>(c)->set_timing(period); }
 void hip_timing(Comm* c, double out[4]) { static_cast<HipComm*>(c)->timing(out); }
 void hip_exchange_timing(Comm* c, double out[3]) { static_cast<HipComm*>(c)->exchange_timing(out); }
+void hip_set_trace(Comm* c, int64_t capacity) { static_cast<HipComm*>(c)->set_trace(capacity); }
+int64_t hip_read_trace(Comm* c, int64_t* out, int64_t capacity) { return static_cast<HipComm*>(c)->read_trace(out, capacity); }
+
+// ---- task trace -------------------------------------------------------------------------
+void HipComm::trace_post(HipWorker& w, int64_t rank) {
+  w.tslot = -1;
+  if (!trace_ || trace_n_ >= trace_cap_) return;
+  w.tslot = trace_n_++;
+  int64_t* e = trace_ + w.tslot * kTraceFields;
+  for (int k = 0; k < kTraceFields; ++k) e[k] = 0;
+  e[kTRank] = rank;
+  e[kTSeq] = int64_t(w.seq);
+  e[kTPost] = int64_t(mono_ns());
+}
+
+void HipComm::gate_seen(int64_t rank, uint64_t seq) {
+  const HipWorker& w = w_[size_t(rank - 1)];
+  int64_t* e = trace_entry(w);
+  if (e && uint64_t(e[kTSeq]) == seq && !e[kTSeen]) e[kTSeen] = int64_t(mono_ns());
+}
+
+// (device ticks, host ns) of one moment: the tightest of 16 launch -> sync round trips of a
+// kernel that stores s_memrealtime, the host time taken as the round trip's midpoint (the
+// error is at most half the round trip, ~10 us: the trace is for millisecond-scale splits)
+void HipComm::calibrate(int64_t* ticks, int64_t* ns) {
+  int64_t best = INT64_MAX;
+  for (int k = 0; k < 16; ++k) {
+    __atomic_store_n(clock_probe_, 0ull, __ATOMIC_SEQ_CST);
+    const int64_t t0 = int64_t(mono_ns());
+    HIPCHECK(launch_clock_probe(reinterpret_cast<unsigned long long*>(clock_probe_), coord_));
+    for (uint64_t spins = 0; __atomic_load_n(clock_probe_, __ATOMIC_ACQUIRE) == 0; ++spins) {
+      if ((spins & 0xFFFF) == 0xFFFF && int64_t(mono_ns()) - t0 > 100000000) {  // 100 ms: a busy stream
+        HIPCHECK(hipStreamSynchronize(coord_));
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    const int64_t t1 = int64_t(mono_ns());
+    if (t1 - t0 < best) {
+      best = t1 - t0;
+      *ticks = int64_t(__atomic_load_n(clock_probe_, __ATOMIC_ACQUIRE));
+      *ns = t0 + (t1 - t0) / 2;
+    }
+    HIPCHECK(hipStreamSynchronize(coord_));
+  }
+}
+
+void HipComm::set_trace(int64_t capacity) {
+  if (capacity < 0) fail(MPA_ARGUMENT_ERROR, "trace capacity < 0");
+  HIPCHECK(hipDeviceSynchronize());  // no task still stamps the old buffer
+  for (auto& w : w_) w.tslot = -1;
+  if (trace_) HIPCHECK(hipHostFree(trace_));
+  trace_ = nullptr;
+  trace_cap_ = trace_n_ = 0;
+  if (capacity == 0) return;
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&trace_), size_t(capacity) * kTraceFields * sizeof(int64_t),
+                         hipHostMallocCoherent | hipHostMallocMapped));
+  if (!clock_probe_)
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&clock_probe_), 64, hipHostMallocCoherent | hipHostMallocMapped));
+  trace_cap_ = capacity;
+  calibrate(&cal_ticks0_, &cal_ns0_);
+}
+
+int64_t HipComm::read_trace(int64_t* out, int64_t capacity) {
+  if (!trace_) return 0;
+  HIPCHECK(hipDeviceSynchronize());
+  int64_t t1 = 0, n1 = 0;
+  calibrate(&t1, &n1);
+  // device ticks -> host ns through the two calibrations (rate and offset)
+  const double rate = t1 > cal_ticks0_ ? double(n1 - cal_ns0_) / double(t1 - cal_ticks0_) : 1e9 / rt_hz_;
+  const int64_t n = trace_n_ < capacity ? trace_n_ : capacity;
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t* e = trace_ + j * kTraceFields;
+    int64_t* o = out + j * kTraceFields;
+    for (int k = 0; k < kTraceFields; ++k) o[k] = e[k];
+    for (int k : {int(kTStart), int(kTPub)})
+      o[k] = e[k] ? cal_ns0_ + int64_t(std::llround(double(e[k] - cal_ticks0_) * rate)) : 0;
+  }
+  return n;
+}
 void hip_serve(Comm* c) { static_cast<HipComm*>(c)->serve(); }
 
 namespace {

@@ -2,7 +2,7 @@
 
 Both bindings are generated from it: the ctypes argtypes of `_capi.py` (the tested Python
 binding) and the low-level `ccall` wrappers of the Julia module
-(`julia/MPIAsyncPoolsHIP/src/capi.jl`, written by `julia/gen_capi.py`).
+(`julia/MPIAsyncPools/src/capi.jl`, written by `julia/gen_capi.py`).
 `tests/test_abi_table.py` checks that the header declares exactly these prototypes and that
 the committed Julia file is what the generator writes, so header, Julia and Python cannot
 drift apart.
@@ -50,6 +50,8 @@ int mpa_comm_payload_path(mpa_comm* comm, int64_t rank);
 int mpa_comm_set_timing(mpa_comm* comm, int enable);
 int mpa_comm_timing(mpa_comm* comm, double out[4]);
 int mpa_comm_exchange_timing(mpa_comm* comm, double out[3]);
+int mpa_comm_set_trace(mpa_comm* comm, int64_t capacity);
+int mpa_comm_trace(mpa_comm* comm, int64_t* out, int64_t capacity, int64_t* count);
 int mpa_comm_sim_set_compute(mpa_comm* comm, int64_t compute_ns);
 int mpa_comm_sim_advance(mpa_comm* comm, int64_t dt_ns);
 int64_t mpa_comm_sim_now(const mpa_comm* comm);

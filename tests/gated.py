@@ -104,6 +104,7 @@ def replay(M, sc, comm, buf, host, predicate, snap=None):
             while time.perf_counter_ns() < t_end:
                 pass
         t0 = time.perf_counter()
+        t0_ns = time.perf_counter_ns()  # CLOCK_MONOTONIC, the transport's steady clock (task trace)
         if op["op"] == "waitall":
             M.waitall_(pool, recv, irecv)
         else:
@@ -114,7 +115,8 @@ def replay(M, sc, comm, buf, host, predicate, snap=None):
         call_ms = (time.perf_counter() - t0) * 1e3
         out.append({"repochs": pool.repochs.tolist(), "sepochs": pool.sepochs.tolist(),
                     "active": pool.active.astype(int).tolist(), "epoch": int(pool.epoch),
-                    "latency_s": pool.latency.tolist(), "recv": snap(recv), "call_ms": call_ms})
+                    "latency_s": pool.latency.tolist(), "recv": snap(recv), "call_ms": call_ms,
+                    "t_ns": (t0_ns, time.perf_counter_ns()), "ranks": list(ranks)})
     for r in out:
         r["recv"] = np.asarray(host(r["recv"])).tolist()
     return out, pool
@@ -153,16 +155,66 @@ def kmap2_replay(M, sc, delays, own_stream=False):
             if delays is not None:
                 comm.set_delays(r, delays[r - 1])
         comm.set_gate(*sched)
+        comm.set_trace(TRACE_CAP)
 
         def buf(k):
             return torch.zeros(k, dtype=torch.float64, device="cuda")
         got, pool = replay(M, sc, comm, buf, lambda t: t.cpu().numpy(), make_golden().predicate,
                            snap=lambda t: t.clone())
         counters = {k: comm.counter(k) for k in ("timer_late", "queues", "shared_worker_streams")}
+        counters["trace"] = comm.trace(TRACE_CAP)
         comm.shutdown()
         comm.close()
         torch.cuda.current_stream().synchronize()
     return got, counters
+
+
+TRACE_CAP = 1 << 14
+F = {k: j for j, k in enumerate(("rank", "seq", "post", "due", "call", "ret", "start", "pub", "seen", "harvest"))}
+LEAD_NS = 35_000  # the transport's default MPA_DELAY_LEAD_NS
+
+
+def task_parts(e):
+    """(ms) where a task's time went against the oracle's clock: timer (the launch call against
+    its due time less the launch lead), launch (the call itself), queue (call returned ->
+    kernel started), kernel, visible (completion store -> the gate saw it), harvest (seen ->
+    taken); `late` = completion store - due (the task's own lateness)."""
+    ms = lambda a, b: round((e[F[a]] - e[F[b]]) / 1e6, 3) if e[F[a]] and e[F[b]] else None
+    due = e[F["due"]]
+    delayed = due - e[F["post"]] > LEAD_NS
+    p = {"task": "r%d#%d" % (e[F["rank"]], e[F["seq"]]),
+         "timer": round((e[F["call"]] - (due - LEAD_NS)) / 1e6, 3) if delayed and e[F["call"]] else None,
+         "launch": ms("ret", "call"), "queue": ms("start", "ret"), "kernel": ms("pub", "start"),
+         "visible": ms("seen", "pub"), "harvest": ms("harvest", "seen"), "late": ms("pub", "due")}
+    return p
+
+
+def explain_misses(got, trace, bad):
+    """For each missed harvest (op k, pool position i): the harvested task's split, and the
+    latest task (completion store - due) the gate waited for during that call."""
+    out = []
+    if trace is None or len(trace) == 0:
+        return out
+    for k, i, d, _tol in bad[:6]:
+        t0, t1 = got[k]["t_ns"]
+        rank = got[k]["ranks"][i]
+        mine = [e for e in trace if e[F["rank"]] == rank and t0 <= e[F["harvest"]] <= t1]
+        during = [e for e in trace if e[F["seen"]] and t0 <= e[F["seen"]] <= t1 and e[F["pub"]]]
+        worst = max(during, key=lambda e: e[F["pub"]] - e[F["due"]], default=None)
+        out.append({"op": k, "pos": i, "dev_ms": d, "harvested": task_parts(mine[-1]) if mine else None,
+                    "latest_in_call": task_parts(worst) if worst is not None else None})
+    return out
+
+
+def trace_stats(trace):
+    """Percentiles (p50 / p99 / max, ms) of each part over every traced task."""
+    parts = [task_parts(e) for e in trace]
+    st = {}
+    for key in ("timer", "launch", "queue", "kernel", "visible", "harvest", "late"):
+        v = np.asarray([p[key] for p in parts if p[key] is not None])
+        if len(v):
+            st[key] = (round(float(np.median(v)), 3), round(float(np.percentile(v, 99)), 3), round(float(v.max()), 3))
+    return st
 
 
 def _child_replay(name, own_stream, q):

@@ -2,7 +2,7 @@
 
   * include/mpiasyncpools.h declares exactly the prototypes of mpiasyncpools/abi.py;
   * the ctypes argtypes the Python binding loads are generated from that table;
-  * julia/MPIAsyncPoolsHIP/src/capi.jl is what julia/gen_capi.py writes from it;
+  * julia/MPIAsyncPools/src/capi.jl is what julia/gen_capi.py writes from it;
   * every mpa_* call of the Julia module names a table entry with the right arity.
 """
 import os
@@ -11,7 +11,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-JL = os.path.join(ROOT, "julia", "MPIAsyncPoolsHIP", "src")
+JL = os.path.join(ROOT, "julia", "MPIAsyncPools", "src")
 
 
 def test_header_matches_table():
@@ -58,7 +58,7 @@ def _calls(src, name):
 def test_julia_module_calls_exist_with_arity():
     from mpiasyncpools import abi
     arity = {name: len(params) for name, _, params in abi.table()}
-    src = open(os.path.join(JL, "MPIAsyncPoolsHIP.jl")).read()
+    src = open(os.path.join(JL, "MPIAsyncPools.jl")).read()
     used = set(re.findall(r"\b(mpa_[a-z0-9_]+)\(", src))
     assert used and used <= set(arity), used - set(arity)
     for name in used:
@@ -83,19 +83,19 @@ def test_julia_mpi_extension_matches_its_header():
     decl = {n: (r, p) for n, r, p in abi.parse(open(os.path.join(ROOT, "include", "mpiasyncpools_mpi.h")).read())}
     assert "mpa_comm_create_mpi" in decl
     ret, params = decl["mpa_comm_create_mpi"]
-    src = open(os.path.join(ROOT, "julia", "MPIAsyncPoolsHIP", "ext", "MPIAsyncPoolsHIPMPIExt.jl")).read()
+    src = open(os.path.join(ROOT, "julia", "MPIAsyncPools", "ext", "MPIAsyncPoolsMPIExt.jl")).read()
     m = re.search(r"ccall\(\(:mpa_comm_create_mpi, libmpi_t\), (\w+), \(([^)]*)\)", src)
     assert m, "the extension ccalls mpa_comm_create_mpi"
     assert m.group(1) == abi.julia_type(ret)
     assert [t.strip() for t in m.group(2).split(",")] == [abi.julia_type(t) for t, _ in params]
-    proj = open(os.path.join(ROOT, "julia", "MPIAsyncPoolsHIP", "Project.toml")).read()
-    assert 'MPIAsyncPoolsHIPMPIExt = "MPI"' in proj
+    proj = open(os.path.join(ROOT, "julia", "MPIAsyncPools", "Project.toml")).read()
+    assert 'MPIAsyncPoolsMPIExt = "MPI"' in proj
 
 
 def test_julia_byte_counts_are_data_bytes():
     """Buffer byte counts handed to the ABI are length * element size (`_nbytes`), never
     `sizeof(buffer)`, which for a wrapper array type is the wrapper's size."""
-    src = open(os.path.join(JL, "MPIAsyncPoolsHIP.jl")).read()
+    src = open(os.path.join(JL, "MPIAsyncPools.jl")).read()
     for name in ("mpa_asyncmap", "mpa_waitall", "mpa_lsq_descent", "mpa_lsqb_descent"):
         for args in _calls(src, name):
             assert not any(re.search(r"\bsizeof\(", a) for a in args), (name, args)

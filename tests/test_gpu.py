@@ -49,6 +49,42 @@ def test_kmap1(M, torch_mod):
     assert isendbuf.cpu().tolist() == [3.14, 3.14]                 # kmap1.jl:30
 
 
+def test_task_trace(M, torch_mod):
+    """mpa_comm_set_trace / mpa_comm_trace: every posted task's life on one clock, in order --
+    post <= due, call <= ret (the timer thread's launch of a delayed task), the kernel's
+    device-clock start <= completion store (mapped to host time; calibration error well under
+    0.1 ms), harvest after the completion; a delayed task's launch call within a few ms of its
+    due time less the launch lead."""
+    torch = torch_mod
+    n = 4
+    comm = M.DeviceComm(n)
+    for r in range(1, n + 1):
+        comm.set_task(r, "kmap2")
+        comm.set_delays(r, [2_000_000 * r, 0])
+    comm.set_trace(64)
+    pool = M.MPIAsyncPool(n)
+    s = torch.ones(1, dtype=torch.float64, device="cuda")
+    rb = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    for _ in range(4):
+        M.asyncmap_(pool, s, rb, torch.zeros(n, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), comm, nwait=n)
+    tr = comm.trace()
+    assert tr.shape == (4 * n, 10)
+    F = {k: j for j, k in enumerate(M.DeviceComm.TRACE_FIELDS)}
+    slack = 100_000  # ns: the device clock's calibration
+    for e in tr:
+        assert 1 <= e[F["rank"]] <= n and e[F["seq"]] >= 1
+        assert 0 < e[F["post"]] <= e[F["due"]] and e[F["post"]] <= e[F["call"]] <= e[F["ret"]]
+        assert e[F["start"]] and e[F["start"]] <= e[F["pub"]] + slack
+        assert e[F["call"]] - slack <= e[F["start"]] and e[F["pub"]] <= e[F["harvest"]] + slack
+        delay = e[F["due"]] - e[F["post"]]
+        if delay:
+            assert delay == 2_000_000 * e[F["rank"]]
+            assert abs(e[F["call"]] - (e[F["due"]] - 35_000)) < 5_000_000
+    comm.set_trace(0)
+    assert len(comm.trace()) == 0
+    comm.shutdown()
+
+
 @pytest.mark.timing
 @pytest.mark.parametrize("nranks", [3, 10])
 def test_kmap2(M, torch_mod, nranks):

@@ -52,12 +52,14 @@ def watchdog():
 def _kmap2_run(M, sc, delays, own_stream=False):
     """One gated replay of a kmap2 scenario in this process (gated.kmap2_replay)."""
     got, counters = gated.kmap2_replay(M, sc, delays, own_stream)
+    _TRACE[0] = counters.pop("trace", None)
     _LAST.clear()
     _LAST.update(counters)
     return got
 
 
 _LAST = {}  # the transport's counters of the last replay (failure messages)
+_TRACE = [None]  # the task trace of the last replay (mpa_comm_trace)
 
 
 def _latency_check(name, sc, got):
@@ -80,6 +82,9 @@ def _latency_check(name, sc, got):
         msg += "; call ms at those ops %s; counters %s; loadavg %s; this process's threads %d" % (
             [(k, round(got[k].get("call_ms", -1.0), 2)) for k in ops], dict(_LAST),
             tuple(round(x, 1) for x in os.getloadavg()), len(os.listdir("/proc/self/task")))
+        msg += "; task trace of the misses %s" % gated.explain_misses(got, _TRACE[0], bad)
+    if _TRACE[0] is not None and len(_TRACE[0]):
+        msg += "; trace p50/p99/max ms %s" % gated.trace_stats(_TRACE[0])
     return not bad and np.median(dev) < 0.2e-3, msg
 
 
@@ -122,6 +127,7 @@ def test_golden_scenario_gated_on_device(M, watchdog, name):
             got = _kmap2_run(M, sc, dur, own_stream=True)
         else:  # in a fresh process: the misses came from the long-lived suite process (r04_gated_stall.txt)
             got, counters = gated.kmap2_replay_in_child(name, own_stream=True)
+            _TRACE[0] = counters.pop("trace", None)
             _LAST.clear()
             _LAST.update(counters)
         assert gated.mismatches(name, got, sc["results"]) == []
