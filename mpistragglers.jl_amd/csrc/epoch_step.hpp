@@ -32,6 +32,12 @@ template <typename T, int V>
 __device__ __forceinline__ EVec<T, V> eld(const T* p) {
   if constexpr (V * sizeof(T) == 16) {
     return __builtin_bit_cast(EVec<T, V>, *reinterpret_cast<const uint4*>(p));
+  } else if constexpr (V * sizeof(T) == 32) {
+    struct U2 {
+      uint4 a, b;
+    };
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    return __builtin_bit_cast(EVec<T, V>, (U2{q[0], q[1]}));
   } else {
     EVec<T, V> r;
 #pragma unroll
@@ -41,10 +47,54 @@ __device__ __forceinline__ EVec<T, V> eld(const T* p) {
 }
 template <typename T, int V>
 __device__ __forceinline__ void est(T* p, const EVec<T, V>& v) {
-  if constexpr (V * sizeof(T) == 16) *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, v);
-  else
+  if constexpr (V * sizeof(T) == 16) {
+    *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, v);
+  } else if constexpr (V * sizeof(T) == 32) {
+    struct U2 {
+      uint4 a, b;
+    };
+    const U2 u = __builtin_bit_cast(U2, v);
+    reinterpret_cast<uint4*>(p)[0] = u.a;
+    reinterpret_cast<uint4*>(p)[1] = u.b;
+  } else {
 #pragma unroll
     for (int e = 0; e < V; ++e) p[e] = v.v[e];
+  }
+}
+
+// V bf16 message elements as ONE store / load: 16 B at V = 8, 8 B at V = 4 (epoch_width
+// guarantees the alignment), element stores otherwise.  A remote worker's message slot is
+// fine-grained memory of another GPU: element stores reached it as 2-byte partial writes
+// (c5 at N = 2 moved 22 GB/s, at N = 8 2.3 GB/s).
+template <int V>
+__device__ __forceinline__ void st_bf16(uint16_t* p, const uint16_t (&h)[V]) {
+  if constexpr (V == 8) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(h[0] | (unsigned(h[1]) << 16), h[2] | (unsigned(h[3]) << 16),
+                                              h[4] | (unsigned(h[5]) << 16), h[6] | (unsigned(h[7]) << 16));
+  } else if constexpr (V == 4) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(h[0] | (unsigned(h[1]) << 16), h[2] | (unsigned(h[3]) << 16));
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e) p[e] = h[e];
+  }
+}
+template <int V>
+__device__ __forceinline__ void ld_bf16(const uint16_t* p, uint16_t (&h)[V]) {
+  if constexpr (V == 8 || V == 4) {
+    unsigned w[V / 2];
+    if constexpr (V == 8) {
+      const uint4 u = *reinterpret_cast<const uint4*>(p);
+      w[0] = u.x, w[1] = u.y, w[2] = u.z, w[3] = u.w;
+    } else {
+      const uint2 u = *reinterpret_cast<const uint2*>(p);
+      w[0] = u.x, w[1] = u.y;
+    }
+#pragma unroll
+    for (int e = 0; e < V / 2; ++e) h[2 * e] = uint16_t(w[e]), h[2 * e + 1] = uint16_t(w[e] >> 16);
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e) h[e] = p[e];
+  }
 }
 
 // relaxed agent-scope element store / load: write-through to the coherence point, visible to
@@ -82,10 +132,11 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
 #pragma unroll
     for (int i = 0; i < kMaxEpochChunks; ++i)
       if (i < a.n && a.hsrc[i]) est<T, V>(recv + int64_t(i) * a.elems + j, c[i]);
+    uint16_t m0[V];  // the bf16 message before the update (held re-dispatches)
+    if (a.msg_bf16 && a.ndst0) ld_bf16<V>(a.mirror + j, m0);
     for (int d = 0; d < a.ndst0; ++d) {  // held re-dispatches: the message before the update
       if (a.msg_bf16) {
-#pragma unroll
-        for (int e = 0; e < V; ++e) reinterpret_cast<uint16_t*>(a.dst0[d])[j + e] = a.mirror[j + e];
+        st_bf16<V>(reinterpret_cast<uint16_t*>(a.dst0[d]) + j, m0);
       } else if constexpr (WT) {
 #pragma unroll
         for (int e = 0; e < V; ++e) st_agent(reinterpret_cast<T*>(a.dst0[d]) + j + e, v.v[e]);
@@ -108,18 +159,21 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
       if (a.hsrc2[i]) est<T, V>(recv + int64_t(i) * a.elems + j, eld<T, V>(reinterpret_cast<const T*>(a.hsrc2[i]) + j));
     if (a.msg_bf16) {  // the message is the bf16 mirror (batched variant): a.mirror != NULL
       uint16_t h[V];
+      if (a.update) {
 #pragma unroll
-      for (int e = 0; e < V; ++e) h[e] = a.update ? f32_to_bf16_rne(float(v.v[e])) : a.mirror[j + e];
-#pragma unroll
-      for (int e = 0; e < V; ++e)
-        if (a.update) a.mirror[j + e] = h[e];
-      for (int d = 0; d < a.ndst; ++d)
-#pragma unroll
-        for (int e = 0; e < V; ++e) reinterpret_cast<uint16_t*>(a.dst[d])[j + e] = h[e];
+        for (int e = 0; e < V; ++e) h[e] = f32_to_bf16_rne(float(v.v[e]));
+        st_bf16<V>(a.mirror + j, h);
+      } else {
+        ld_bf16<V>(a.mirror + j, h);
+      }
+      for (int d = 0; d < a.ndst; ++d) st_bf16<V>(reinterpret_cast<uint16_t*>(a.dst[d]) + j, h);
     } else {
-      if (a.update && a.mirror)
+      if (a.update && a.mirror) {
+        uint16_t h[V];
 #pragma unroll
-        for (int e = 0; e < V; ++e) a.mirror[j + e] = f32_to_bf16_rne(float(v.v[e]));
+        for (int e = 0; e < V; ++e) h[e] = f32_to_bf16_rne(float(v.v[e]));
+        st_bf16<V>(a.mirror + j, h);
+      }
       for (int d = 0; d < a.ndst; ++d) {
         if constexpr (WT) {
 #pragma unroll

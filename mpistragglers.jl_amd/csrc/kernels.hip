@@ -330,35 +330,36 @@ hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// 16-B vectors when the element count and every pointer the kernel touches allow it
-bool epoch_vec(int dtype, const EpochArgs& a) {
-  const int V = dtype == MPA_F64 ? 2 : 4;
+// Elements per thread of the epoch step: 16-B vectors of the iterate (4 fp32 / 2 fp64) when
+// the element count and every pointer the kernel touches allow it; fp32 with bf16 messages
+// (the batched variant) takes 8, so each message store is one 16-B vector (4: 8 B).
+int epoch_width(int dtype, const EpochArgs& a) {
   uintptr_t m = reinterpret_cast<uintptr_t>(a.recv) | reinterpret_cast<uintptr_t>(a.x);
   for (int i = 0; i < a.n; ++i)
     m |= reinterpret_cast<uintptr_t>(a.hsrc[i]) | reinterpret_cast<uintptr_t>(a.hsrc2[i]);
-  if (a.msg_bf16 || a.mirror) {
-    m |= reinterpret_cast<uintptr_t>(a.mirror) & 7u;  // 4 bf16 per thread (8 B)
-    for (int d = 0; d < a.ndst; ++d) m |= reinterpret_cast<uintptr_t>(a.dst[d]) & 7u;
-    for (int d = 0; d < a.ndst0; ++d) m |= reinterpret_cast<uintptr_t>(a.dst0[d]) & 7u;
-  }
-  if (!a.msg_bf16) {
-    for (int d = 0; d < a.ndst; ++d) m |= reinterpret_cast<uintptr_t>(a.dst[d]);
-    for (int d = 0; d < a.ndst0; ++d) m |= reinterpret_cast<uintptr_t>(a.dst0[d]);
-  }
-  return a.elems % V == 0 && (m & 15u) == 0;
+  uintptr_t mb = reinterpret_cast<uintptr_t>(a.mirror);  // bf16 stores
+  for (int d = 0; d < a.ndst; ++d) (a.msg_bf16 ? mb : m) |= reinterpret_cast<uintptr_t>(a.dst[d]);
+  for (int d = 0; d < a.ndst0; ++d) (a.msg_bf16 ? mb : m) |= reinterpret_cast<uintptr_t>(a.dst0[d]);
+  if (dtype == MPA_F64) return a.elems % 2 == 0 && (m & 15u) == 0 && (mb & 3u) == 0 ? 2 : 1;
+  if (a.msg_bf16 && a.elems % 8 == 0 && ((m | mb) & 15u) == 0) return 8;
+  return a.elems % 4 == 0 && (m & 15u) == 0 && (mb & 7u) == 0 ? 4 : 1;
 }
 
+bool epoch_vec(int dtype, const EpochArgs& a) { return epoch_width(dtype, a) > 1; }
+
 int epoch_grid(int dtype, const EpochArgs& a) {
-  const int V = epoch_vec(dtype, a) ? (dtype == MPA_F64 ? 2 : 4) : 1;
+  const int V = epoch_width(dtype, a);
   const int64_t g = (a.elems / V + kThreads - 1) / kThreads;
   return int(g < 1 ? 1 : g > 1024 ? 1024 : g);
 }
 
 hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s) {
   const int grid = epoch_grid(dtype, a);
-  const bool vec = epoch_vec(dtype, a);
+  const int width = epoch_width(dtype, a);
+  const bool vec = width > 1;
   if (dtype == MPA_F32) {
-    if (vec) hipLaunchKernelGGL((epoch_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (width == 8) hipLaunchKernelGGL((epoch_kernel<float, 8>), dim3(grid), dim3(kThreads), 0, s, a);
+    else if (vec) hipLaunchKernelGGL((epoch_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL((epoch_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   } else if (dtype == MPA_F64) {
     if (vec) hipLaunchKernelGGL((epoch_kernel<double, 2>), dim3(grid), dim3(kThreads), 0, s, a);

@@ -396,6 +396,7 @@ hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s);
 int epoch_grid(int dtype, const EpochArgs& a);
 // the step can use 16-B vectors (element count and every pointer allow it)
 bool epoch_vec(int dtype, const EpochArgs& a);
+int epoch_width(int dtype, const EpochArgs& a);  // elements per thread: 1, 2 / 4 (16-B vectors), 8 (bf16 messages)
 hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s);
 
 // streaming read of `bytes` (a multiple of 16) for the measured HBM read ceiling; `sink`

@@ -430,3 +430,118 @@ def lsq_descent_dist(rank, world, port, placement, env, result_q):
     except Exception:
         result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
         raise
+
+
+SCHED_CONFIGS = {
+    # BASELINE configs[2] (c3): fp32, nwait 6 of 8, stale results dropped; configs[3] (c4): fp64,
+    # worker 1 fresh + 5 others (mpa_nwait_first_plus), stale results at weight 0.5
+    "c3": dict(scenario="gpu_sep_c3", dt="f32", nwait=6, stale=0.0, tol=1e-5, seed=43),
+    "c4": dict(scenario="gpu_sep_c4_first_plus_5", dt="f64", nwait="first_plus5", stale=0.5, tol=1e-12, seed=41),
+}
+
+
+def lsq_sched_dist(rank, world, port, placement, config, epoch0, result_q):
+    """BASELINE c3 / c4 in the node's placement (rank 0 coordinates and serves worker 1, ranks
+    1-7 serve one worker each), on the oracle's golden schedule: every worker process injects
+    the schedule's durations as its task delays (so its tasks are host-launched by its serve
+    loop's timer, not device-armed), and rank 0 runs the Python-driven coordinator loop under the
+    oracle's gate (tests/gated.py), checking what tests/test_gpu_configs.py checks in one
+    process: repochs / active after every asyncmap! equal the oracle's, every chunk i equals the
+    fp64 gradient of the iterate sent at epoch repochs[i] (1e-5 fp32 / 1e-12 fp64), the iterate
+    equals a numpy replay of the update (fresh weight 1, stale `stale`, never heard from 0,
+    scaled by n / sum(w))."""
+    import numpy as np
+    try:
+        dist = _init(rank, world, port)
+        import torch
+        torch.cuda.set_device(0)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import gated
+        import lsq
+        import mpiasyncpools as M
+        cfg = SCHED_CONFIGS[config]
+        sc = next(s for s in gated.scenarios() if s["name"] == cfg["scenario"])
+        n, rows, cols, eta = sc["n"], 512, 2048, 0.2
+        assert n == len(placement)
+        es = 8 if cfg["dt"] == "f64" else 4
+        tdt = torch.float64 if cfg["dt"] == "f64" else torch.float32
+        name = [f"/mpa_s{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+        if rank == 0:
+            comm = M.DistComm(n, placement, 0, name[0], cols * es, transport="hip")
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            comm = M.DistComm(n, placement, rank, name[0], cols * es, transport="hip")
+        dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(n, -1)
+        keep = []
+        for w in range(1, n + 1):
+            if placement[w - 1] == rank:
+                A = lsq.gen_matrix(cfg["seed"], (w - 1) * rows, rows, cols, cfg["dt"])
+                b = lsq.gen_vector(cfg["seed"], (w - 1) * rows, rows, cfg["dt"])
+                keep.append((torch.from_numpy(A).cuda(), torch.from_numpy(b).cuda()))
+                comm.set_task_lsq(w, *keep[-1])
+                comm.set_delays(w, dur[w - 1])
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank != 0:
+            comm.serve()
+            dist.barrier()
+            comm.close()
+            dist.destroy_process_group()
+            return
+        A_all, b_all = lsq.gen_matrix(cfg["seed"], 0, n * rows, cols, cfg["dt"]), lsq.gen_vector(cfg["seed"], 0, n * rows, cfg["dt"])
+        comm.set_gate(*gated.oracle_gate(sc)[1])
+        nwait = M.first_plus(5) if cfg["nwait"] == "first_plus5" else cfg["nwait"]
+        pool = M.MPIAsyncPool(n, epoch0=epoch0)
+        x = torch.zeros(cols, dtype=tdt, device="cuda")
+        isend = torch.zeros(n * cols, dtype=tdt, device="cuda")
+        recv = torch.zeros(n * cols, dtype=tdt, device="cuda")
+        irecv = torch.zeros_like(recv)
+        errors, sent, got, reps, ws = [], {}, [], [], []
+        steps = [(op, ref) for op, ref in zip(sc["ops"], sc["results"]) if op["op"] == "asyncmap"]
+        for k, (op, ref) in enumerate(steps):
+            epoch = epoch0 + k + 1
+            sent[epoch] = x.clone()
+            rep = M.asyncmap_(pool, x, recv, isend, irecv, comm, nwait=nwait).copy()
+            ref_rep = [r + epoch0 for r in ref["repochs"]]  # the oracle runs at epoch0 = 0
+            if rep.tolist() != ref_rep or pool.active.astype(int).tolist() != ref["active"]:
+                errors.append(("trace", k, rep.tolist(), ref_rep, pool.active.astype(int).tolist(), ref["active"]))
+            got.append(recv.clone())
+            w = np.zeros(n)
+            for i in range(n):
+                if ref["repochs"][i] != 0:  # never heard from: chunk unfilled, weight 0
+                    w[i] = 1.0 if rep[i] == epoch else cfg["stale"]
+            w *= n / w.sum() if w.sum() > 0 else 0.0
+            comm.lsq_update(x, recv, n, w, eta)
+            reps.append(rep)
+            ws.append(w)
+        M.waitall_(pool, recv, irecv)
+        torch.cuda.synchronize()
+        paths = [comm.payload_path(w) for w in range(1, n + 1) if placement[w - 1] != 0]
+        if paths != ["device"] * len(paths):
+            errors.append(("payload path", paths))
+        comm.shutdown()
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        tol = cfg["tol"]
+        sent = {e: v.cpu().numpy().astype(np.float64) for e, v in sent.items()}
+        x_np = np.zeros(cols)
+        for k, (rep, w, r) in enumerate(zip(reps, ws, got)):
+            epoch = epoch0 + k + 1
+            if not (np.array_equal(sent[epoch], x_np) or lsq.rel_err(sent[epoch], x_np) <= tol):
+                errors.append(("iterate", k, lsq.rel_err(sent[epoch], x_np)))
+            chunks = r.cpu().numpy().reshape(n, cols).astype(np.float64)
+            for i in range(n):
+                if rep[i] - epoch0 == 0:
+                    continue
+                g = lsq.shard_gradient(A_all[i * rows:(i + 1) * rows], b_all[i * rows:(i + 1) * rows], sent[int(rep[i])])
+                e = lsq.rel_err(chunks[i], g)
+                if not e <= tol:
+                    errors.append(("chunk", k, i, int(rep[i]), e))
+            x_np = x_np - eta * (w[:, None] * chunks).sum(0)
+        if lsq.rel_err(x.cpu().numpy().astype(np.float64), x_np) > tol:
+            errors.append(("final iterate", lsq.rel_err(x.cpu().numpy().astype(np.float64), x_np)))
+        result_q.put(("ok", errors))
+    except Exception:
+        result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
+        raise

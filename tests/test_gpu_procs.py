@@ -118,3 +118,17 @@ def test_lsq_descent_two_processes(built, placement, env):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run(dist_worker.lsq_descent_dist, 2, placement, env)
+
+
+@pytest.mark.parametrize("config,epoch0", [("c3", 0), ("c4", 0), ("c4", 1000)])
+def test_sched_eight_processes(built, config, epoch0):
+    """BASELINE c3 (nwait 6 of 8, fp32) and c4 (fp64, worker 1 fresh + 5 others, stale results
+    at weight 0.5) in the node's placement -- rank 0 plus seven one-worker processes, all on
+    GPU 0 here -- on the oracle's golden schedule injected as the workers' delays and gated on
+    rank 0: the oracle's repochs / active after every call, every chunk the gradient of the
+    iterate sent at its epoch (1e-5 / 1e-12), the iterate equal to the numpy replay
+    (dist_worker.lsq_sched_dist; one process: tests/test_gpu_configs.py)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.lsq_sched_dist, 8, list(range(8)), config, epoch0, timeout=240)
