@@ -67,33 +67,29 @@ __device__ __forceinline__ void est(T* p, const EVec<T, V>& v) {
 // fine-grained memory of another GPU: element stores reached it as 2-byte partial writes
 // (c5 at N = 2 moved 22 GB/s, at N = 8 2.3 GB/s).
 template <int V>
-__device__ __forceinline__ void st_bf16(uint16_t* p, const uint16_t (&h)[V]) {
+using H16 = EVec<uint16_t, V>;
+template <int V>
+__device__ __forceinline__ void st_bf16(uint16_t* p, const H16<V> h) {
   if constexpr (V == 8) {
-    *reinterpret_cast<uint4*>(p) = make_uint4(h[0] | (unsigned(h[1]) << 16), h[2] | (unsigned(h[3]) << 16),
-                                              h[4] | (unsigned(h[5]) << 16), h[6] | (unsigned(h[7]) << 16));
+    *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, h);
   } else if constexpr (V == 4) {
-    *reinterpret_cast<uint2*>(p) = make_uint2(h[0] | (unsigned(h[1]) << 16), h[2] | (unsigned(h[3]) << 16));
+    *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, h);
   } else {
 #pragma unroll
-    for (int e = 0; e < V; ++e) p[e] = h[e];
+    for (int e = 0; e < V; ++e) p[e] = h.v[e];
   }
 }
 template <int V>
-__device__ __forceinline__ void ld_bf16(const uint16_t* p, uint16_t (&h)[V]) {
-  if constexpr (V == 8 || V == 4) {
-    unsigned w[V / 2];
-    if constexpr (V == 8) {
-      const uint4 u = *reinterpret_cast<const uint4*>(p);
-      w[0] = u.x, w[1] = u.y, w[2] = u.z, w[3] = u.w;
-    } else {
-      const uint2 u = *reinterpret_cast<const uint2*>(p);
-      w[0] = u.x, w[1] = u.y;
-    }
-#pragma unroll
-    for (int e = 0; e < V / 2; ++e) h[2 * e] = uint16_t(w[e]), h[2 * e + 1] = uint16_t(w[e] >> 16);
+__device__ __forceinline__ H16<V> ld_bf16(const uint16_t* p) {
+  if constexpr (V == 8) {
+    return __builtin_bit_cast(H16<V>, *reinterpret_cast<const uint4*>(p));
+  } else if constexpr (V == 4) {
+    return __builtin_bit_cast(H16<V>, *reinterpret_cast<const uint2*>(p));
   } else {
+    H16<V> h;
 #pragma unroll
-    for (int e = 0; e < V; ++e) h[e] = p[e];
+    for (int e = 0; e < V; ++e) h.v[e] = p[e];
+    return h;
   }
 }
 
@@ -115,7 +111,9 @@ __device__ __forceinline__ T ld_agent(const T* p) {
 // n read x, a valid address, and are ignored): a load under a branch made the compiler wait
 // for each one in turn.
 // WT: the dispatch copies are stored write-through (st_agent; the fused head, not bf16 messages)
-template <typename T, int V, bool WT = false>
+// BF16 = false: the caller never passes bf16 messages or a mirror (the fused tail / head of the
+// least-squares launch, transport_hip.cpp tail_fits / fused_head), so that code is left out
+template <typename T, int V, bool WT = false, bool BF16 = true>
 __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, int64_t stride) {
   T* recv = reinterpret_cast<T*>(a.recv);
   T* x = static_cast<T*>(a.x);
@@ -132,11 +130,9 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
 #pragma unroll
     for (int i = 0; i < kMaxEpochChunks; ++i)
       if (i < a.n && a.hsrc[i]) est<T, V>(recv + int64_t(i) * a.elems + j, c[i]);
-    uint16_t m0[V];  // the bf16 message before the update (held re-dispatches)
-    if (a.msg_bf16 && a.ndst0) ld_bf16<V>(a.mirror + j, m0);
     for (int d = 0; d < a.ndst0; ++d) {  // held re-dispatches: the message before the update
-      if (a.msg_bf16) {
-        st_bf16<V>(reinterpret_cast<uint16_t*>(a.dst0[d]) + j, m0);
+      if (BF16 && a.msg_bf16) {
+        st_bf16<V>(reinterpret_cast<uint16_t*>(a.dst0[d]) + j, ld_bf16<V>(a.mirror + j));
       } else if constexpr (WT) {
 #pragma unroll
         for (int e = 0; e < V; ++e) st_agent(reinterpret_cast<T*>(a.dst0[d]) + j + e, v.v[e]);
@@ -157,21 +153,21 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
     }
     for (int i = 0; i < a.n; ++i)
       if (a.hsrc2[i]) est<T, V>(recv + int64_t(i) * a.elems + j, eld<T, V>(reinterpret_cast<const T*>(a.hsrc2[i]) + j));
-    if (a.msg_bf16) {  // the message is the bf16 mirror (batched variant): a.mirror != NULL
-      uint16_t h[V];
+    if (BF16 && a.msg_bf16) {  // the message is the bf16 mirror (batched variant): a.mirror != NULL
+      H16<V> h;
       if (a.update) {
 #pragma unroll
-        for (int e = 0; e < V; ++e) h[e] = f32_to_bf16_rne(float(v.v[e]));
+        for (int e = 0; e < V; ++e) h.v[e] = f32_to_bf16_rne(float(v.v[e]));
         st_bf16<V>(a.mirror + j, h);
       } else {
-        ld_bf16<V>(a.mirror + j, h);
+        h = ld_bf16<V>(a.mirror + j);
       }
       for (int d = 0; d < a.ndst; ++d) st_bf16<V>(reinterpret_cast<uint16_t*>(a.dst[d]) + j, h);
     } else {
-      if (a.update && a.mirror) {
-        uint16_t h[V];
+      if (BF16 && a.update && a.mirror) {
+        H16<V> h;
 #pragma unroll
-        for (int e = 0; e < V; ++e) h[e] = f32_to_bf16_rne(float(v.v[e]));
+        for (int e = 0; e < V; ++e) h.v[e] = f32_to_bf16_rne(float(v.v[e]));
         st_bf16<V>(a.mirror + j, h);
       }
       for (int d = 0; d < a.ndst; ++d) {

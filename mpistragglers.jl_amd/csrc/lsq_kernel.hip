@@ -226,12 +226,12 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
         const uint4* src = s_go == 2 ? reinterpret_cast<const uint4*>(&batch.ep) : reinterpret_cast<const uint4*>(batch.pre_ep);
         for (int k = tid; k < kEpVecs; k += kThreads) reinterpret_cast<uint4*>(&s_ep)[k] = src[k];
         __syncthreads();
-        if ((batch.head & 3) == 2) epoch_elems<T, E, true>(s_ep, tid, kThreads);
-        else epoch_elems<T, 1, true>(s_ep, tid, kThreads);
+        if ((batch.head & 3) == 2) epoch_elems<T, E, true, false>(s_ep, tid, kThreads);
+        else epoch_elems<T, 1, true, false>(s_ep, tid, kThreads);
       } else if ((batch.head & 3) == 2) {
-        epoch_elems<T, E, true>(batch.ep, tid, kThreads);
+        epoch_elems<T, E, true, false>(batch.ep, tid, kThreads);
       } else {
-        epoch_elems<T, 1, true>(batch.ep, tid, kThreads);
+        epoch_elems<T, 1, true, false>(batch.ep, tid, kThreads);
       }
       drain_vm();
       __syncthreads();
@@ -493,8 +493,8 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   } else {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
-  if (batch.tail == 2) epoch_elems<T, E>(batch.ep, tid, kThreads);
-  else epoch_elems<T, 1>(batch.ep, tid, kThreads);
+  if (batch.tail == 2) epoch_elems<T, E, false, false>(batch.ep, tid, kThreads);
+  else epoch_elems<T, 1, false, false>(batch.ep, tid, kThreads);
   if (batch.ep.ndoor == 0) return;
   // the next messages of remote workers are in their slots: release them at system scope,
   // then ring the doorbells (as epoch_kernel's last block)
