@@ -523,7 +523,7 @@ def run_multi(args, cfg, rank, world, local):
     torch.cuda.set_device(0 if one_gpu else local)
     dist.init_process_group("gloo")
     n = cfg["workers"]
-    placement = [(w * world) // n for w in range(n)]  # 8/N consecutive workers per rank
+    placement = bench_placement(n, world)
     name = [f"/mpa_bench_{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
     if rank == 0:
         comm = M.DistComm(n, placement, 0, name[0], max_msg_bytes(cfg))
@@ -570,17 +570,30 @@ def run_multi(args, cfg, rank, world, local):
     xch = exchange_report(comm.exchange_timing()) if rank == 0 else None
     dist.barrier()
     stats = [None] * world
-    dist.all_gather_object(stats, (el, timing))
+    dist.all_gather_object(stats, (el, timing, os.getpid()))
     if rank == 0:
         el_max = max(s[0] for s in stats)
         paths = sorted({comm.payload_path(w) for w in range(1, n + 1) if placement[w - 1] != 0} - {None})
         extra = {"x_norm": float(torch.linalg.norm(x.float()).item()), "build": M.lib().mpa_build_info().decode(),
                  "fresh_at_last_epoch": fresh, "placement": placement, "payload_path": "/".join(paths) or None, "rank0_elapsed_s": round(stats[0][0], 6), "cpu_baseline": None,
-                 "exchange": xch}
+                 "exchange": xch, "rank_pids": [s[2] for s in stats]}
         print(json.dumps(report(args, cfg, world, el_max, [s[1] for s in stats], extra)), flush=True)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()
+
+
+def bench_placement(n, world):
+    """8/N consecutive workers per rank; MPA_BENCH_PLACEMENT (rehearsals only, e.g. "0,0,0,0,0,0,0,1":
+    rank 0 serves seven workers and rank 1 one, the per-remote-worker control path of the 8-GPU
+    node's placement on a one-GPU box) overrides it."""
+    env = os.environ.get("MPA_BENCH_PLACEMENT")
+    if env:
+        pl = [int(v) for v in env.split(",")]
+        if len(pl) != n or sorted(set(pl)) != list(range(world)):
+            raise SystemExit(f"MPA_BENCH_PLACEMENT {env!r}: {n} ranks in 0..{world - 1}, each used")
+        return pl
+    return [(w * world) // n for w in range(n)]
 
 
 def run_dry(args, cfg, rank, world):

@@ -243,14 +243,15 @@ int mpa_comm_timing(mpa_comm* comm, double out[4]);
 int mpa_comm_exchange_timing(mpa_comm* comm, double out[3]);
 /* HIP transport, diagnostics: the task trace.  mpa_comm_set_trace(comm, capacity) starts a
  * trace of the next `capacity` posted tasks (0: off; the previous trace is dropped).
- * mpa_comm_trace copies min(count recorded, capacity) entries of 10 int64 each into `out`:
- * {rank, seq, post, due, call, ret, start, pub, seen, harvest}, host steady-clock ns, 0 where
+ * mpa_comm_trace copies min(count recorded, capacity) entries of 11 int64 each into `out`:
+ * {rank, seq, post, due, call, ret, start, pub, gate, seen, harvest}, host steady-clock ns, 0 where
  * the task did not reach that point: post = dispatch (src/MPIAsyncPools.jl:130-137), due =
  * post + its injected delay (the reference worker's reply time), call / ret = the launch call
  * of its kernel entered / returned (the timer thread's for a delayed task), start / pub = the
  * kernel's first instruction and its completion store on the device clock (s_memrealtime,
- * mapped to host time by clock calibrations; the reference's worker programs only), seen = a
- * gated replay observed the completion, harvest = phase 1 or the wait loop took it
+ * mapped to host time by clock calibrations; the reference's worker programs only), gate / seen = a
+ * gated replay's step that waited for it began / observed the completion, harvest = phase 1 or
+ * the wait loop took it
  * (:99-104, :161-167).  A late harvest splits into launch call, queue, kernel, visibility. */
 int mpa_comm_set_trace(mpa_comm* comm, int64_t capacity);
 int mpa_comm_trace(mpa_comm* comm, int64_t* out, int64_t capacity, int64_t* count);

@@ -105,8 +105,13 @@ class Comm {
   virtual uint64_t gate_finished(int64_t rank) { (void)rank; return 0; }
   virtual void gate_launch(int64_t rank) { (void)rank; }
   virtual void gate_poll(double waited_s) { (void)waited_s; }
-  // the gate saw task `seq` of `rank` complete (task trace, HipComm)
-  virtual void gate_seen(int64_t rank, uint64_t seq) { (void)rank; (void)seq; }
+  // the gate step that began at step_begin_ns (steady clock) saw task `seq` of `rank` complete
+  // (task trace, HipComm)
+  virtual void gate_seen(int64_t rank, uint64_t seq, uint64_t step_begin_ns) {
+    (void)rank;
+    (void)seq;
+    (void)step_begin_ns;
+  }
 
   int64_t nworkers_;
   std::vector<TaskSpec> tasks_;

@@ -67,6 +67,7 @@ void Comm::gate(int kind) {
     gate_launch(r);
   }
   const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t t0_ns = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count());
   for (int64_t j = a; j < e; ++j) {
     const int64_t r = gate_ranks_[size_t(j)];
     for (uint64_t spins = 0; gate_finished(r) < gate_rel_[size_t(r - 1)]; ++spins) {
@@ -74,7 +75,7 @@ void Comm::gate(int kind) {
         gate_poll(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
       std::this_thread::yield();
     }
-    gate_seen(r, gate_rel_[size_t(r - 1)]);
+    gate_seen(r, gate_rel_[size_t(r - 1)], t0_ns);
   }
   ++gate_step_;
 }

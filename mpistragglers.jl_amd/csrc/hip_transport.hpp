@@ -650,14 +650,15 @@ class HipComm final : public Comm {
   // the oracle's completion time), call / ret (the launch call of the task kernel: entered,
   // returned -- the timer thread's for a delayed task), start / pub (the kernel's first
   // instruction and its completion store, read on the device's s_memrealtime and mapped to
-  // host time by two clock calibrations), seen (the gate observed the completion), harvest
-  // (phase 1 / wait loop took it).  Stamps are written for the reference's worker programs
-  // (kmap tasks); least-squares tasks get the host fields only.
-  static constexpr int kTraceFields = 10;
-  enum TraceField { kTRank, kTSeq, kTPost, kTDue, kTCall, kTRet, kTStart, kTPub, kTSeen, kTHarvest };
+  // host time by two clock calibrations), gate (the gate step that waits for it began), seen
+  // (the gate observed the completion), harvest (phase 1 / wait loop took it).  Stamps are
+  // written for the reference's worker programs (kmap tasks); least-squares tasks get the host
+  // fields only.
+  static constexpr int kTraceFields = 11;
+  enum TraceField { kTRank, kTSeq, kTPost, kTDue, kTCall, kTRet, kTStart, kTPub, kTGate, kTSeen, kTHarvest };
   void set_trace(int64_t capacity);
   int64_t read_trace(int64_t* out, int64_t capacity);
-  void gate_seen(int64_t rank, uint64_t seq) override;
+  void gate_seen(int64_t rank, uint64_t seq, uint64_t step_begin_ns) override;
 
  private:
   int64_t* trace_ = nullptr;  // host-pinned, capacity x kTraceFields

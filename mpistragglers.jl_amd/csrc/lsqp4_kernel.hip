@@ -41,6 +41,10 @@
 // C/D[m=4g+r][n=i]; lane l: i = l & 15, g = l >> 4.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "mpiasyncpools.h"
@@ -182,6 +186,15 @@ __device__ __forceinline__ f32x4 ld_wt(const f32x4* p) {
   u[1] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return __builtin_bit_cast(f32x4, u);
 }
+
+#if MPA_MEASURE
+// In-kernel clock (measurement build only; MI355X_MICROARCH.md 'DVFS give-back' item 6): thread 0
+// of every workgroup stamps s_memtime (shader cycles) and s_memrealtime (100 MHz) once before and
+// once after its block loop; the last launch's stamps are read by lsqp4_clock_dump() (MPA_LSQP4_CLOCK=1,
+// at comm teardown).  Nothing in the kernel reads them.
+constexpr int kClockSlots = 4096;
+__device__ unsigned long long g_lsqp4_clk[kClockSlots][4];
+#endif
 
 // FULL: every task of the batch has cols == 2048 and rows % 16 == 0 (BASELINE c5's shape):
 // no ragged block, no partial strip, so the block loop drops the clamps, selects and masks
@@ -617,10 +630,26 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     }
     pf(kb0 + u + 2 + pfd);
   };
+#if MPA_MEASURE
+  unsigned long long clk0 = 0, rt0 = 0;
+  if (tid == 0) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   for (int u = 0; u < nb; u += 2) {
     step(u, my0, bring[0], part[0]);
     if (u + 1 < nb) step(u + 1, my1, bring[1], part[1]);
   }
+#if MPA_MEASURE
+  if (tid == 0 && bx < kClockSlots) {
+    const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    g_lsqp4_clk[bx][0] = clk0;
+    g_lsqp4_clk[bx][1] = rt0;
+    g_lsqp4_clk[bx][2] = clk1;
+    g_lsqp4_clk[bx][3] = rt1;
+  }
+#endif
 #undef MPA_VMCNT
   drain_vm();  // the trailing (unused) DMA pieces
 
@@ -700,6 +729,24 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
 }
 
 }  // namespace
+
+#if MPA_MEASURE
+void lsqp4_clock_dump() {
+  static unsigned long long h[kClockSlots][4];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_lsqp4_clk), sizeof(h)) != hipSuccess) return;
+  std::vector<double> ghz, us;
+  for (int b = 0; b < kClockSlots; ++b)
+    if (h[b][3] > h[b][1] && h[b][2] > h[b][0]) {
+      ghz.push_back(double(h[b][2] - h[b][0]) / double(h[b][3] - h[b][1]) * 0.1);  // 100 MHz realtime
+      us.push_back(double(h[b][3] - h[b][1]) / 100.0);
+    }
+  if (ghz.empty()) return;
+  std::sort(ghz.begin(), ghz.end());
+  std::sort(us.begin(), us.end());
+  std::fprintf(stderr, "lsqp4 clock: %zu workgroups, in-kernel clock median %.3f GHz (min %.3f, max %.3f), block loop median %.1f us\n",
+               ghz.size(), ghz[ghz.size() / 2], ghz.front(), ghz.back(), us[us.size() / 2]);
+}
+#endif
 
 hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s) {
   const int pairs = a.grp0[a.ntasks];

@@ -166,6 +166,7 @@ HipComm::~HipComm() {
   (void)hipDeviceSynchronize();
 #if MPA_MEASURE
   if (const char* d = measure_env("MPA_LSQF_DBG"); d && (std::atoi(d) & 16)) lsqf_prof_dump();
+  if (const char* d = measure_env("MPA_LSQP4_CLOCK"); d && *d == '1') lsqp4_clock_dump();
 #endif
   for (auto& w : w_) {
     if (w.slab) (void)hipFree(w.slab);
@@ -886,10 +887,13 @@ void HipComm::trace_post(HipWorker& w, int64_t rank) {
   e[kTPost] = int64_t(mono_ns());
 }
 
-void HipComm::gate_seen(int64_t rank, uint64_t seq) {
+void HipComm::gate_seen(int64_t rank, uint64_t seq, uint64_t step_begin_ns) {
   const HipWorker& w = w_[size_t(rank - 1)];
   int64_t* e = trace_entry(w);
-  if (e && uint64_t(e[kTSeq]) == seq && !e[kTSeen]) e[kTSeen] = int64_t(mono_ns());
+  if (e && uint64_t(e[kTSeq]) == seq && !e[kTSeen]) {
+    e[kTGate] = int64_t(step_begin_ns);
+    e[kTSeen] = int64_t(mono_ns());
+  }
 }
 
 // (device ticks, host ns) of one moment: the tightest of 16 launch -> sync round trips of a

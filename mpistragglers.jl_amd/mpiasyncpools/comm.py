@@ -192,14 +192,14 @@ class DeviceComm(_Comm):
         check(lib().mpa_comm_exchange_timing(self._h, out))
         return int(out[0]), float(out[1]), float(out[2])
 
-    TRACE_FIELDS = ("rank", "seq", "post", "due", "call", "ret", "start", "pub", "seen", "harvest")
+    TRACE_FIELDS = ("rank", "seq", "post", "due", "call", "ret", "start", "pub", "gate", "seen", "harvest")
 
     def set_trace(self, capacity):
         """Trace the next `capacity` posted tasks (mpa_comm_set_trace; 0 = off)."""
         check(lib().mpa_comm_set_trace(self._h, int(capacity)))
 
     def trace(self, capacity=1 << 16):
-        """The task trace as an int64 array (tasks x 10, columns TRACE_FIELDS, host ns)."""
+        """The task trace as an int64 array (tasks x 11, columns TRACE_FIELDS, host ns)."""
         out = np.zeros((int(capacity), len(self.TRACE_FIELDS)), dtype=np.int64)
         n = C.c_int64(0)
         check(lib().mpa_comm_trace(self._h, out.ctypes.data_as(C.POINTER(C.c_int64)), int(capacity), C.byref(n)))

@@ -170,22 +170,25 @@ def kmap2_replay(M, sc, delays, own_stream=False):
 
 
 TRACE_CAP = 1 << 14
-F = {k: j for j, k in enumerate(("rank", "seq", "post", "due", "call", "ret", "start", "pub", "seen", "harvest"))}
+F = {k: j for j, k in enumerate(("rank", "seq", "post", "due", "call", "ret", "start", "pub", "gate", "seen", "harvest"))}
 LEAD_NS = 35_000  # the transport's default MPA_DELAY_LEAD_NS
 
 
 def task_parts(e):
     """(ms) where a task's time went against the oracle's clock: timer (the launch call against
     its due time less the launch lead), launch (the call itself), queue (call returned ->
-    kernel started), kernel, visible (completion store -> the gate saw it), harvest (seen ->
-    taken); `late` = completion store - due (the task's own lateness)."""
+    kernel started), kernel, visible (completion store, or the gate step's start if that came
+    later -> the gate saw it: the coordinator's own lateness), harvest (seen -> taken); `late` =
+    completion store - due (the task's own lateness)."""
     ms = lambda a, b: round((e[F[a]] - e[F[b]]) / 1e6, 3) if e[F[a]] and e[F[b]] else None
     due = e[F["due"]]
     delayed = due - e[F["post"]] > LEAD_NS
     p = {"task": "r%d#%d" % (e[F["rank"]], e[F["seq"]]),
          "timer": round((e[F["call"]] - (due - LEAD_NS)) / 1e6, 3) if delayed and e[F["call"]] else None,
          "launch": ms("ret", "call"), "queue": ms("start", "ret"), "kernel": ms("pub", "start"),
-         "visible": ms("seen", "pub"), "harvest": ms("harvest", "seen"), "late": ms("pub", "due")}
+         "visible": (round((e[F["seen"]] - max(e[F["pub"]], e[F["gate"]])) / 1e6, 3)
+                     if e[F["seen"]] and e[F["pub"]] else None),
+         "harvest": ms("harvest", "seen"), "late": ms("pub", "due")}
     return p
 
 

@@ -68,7 +68,7 @@ def test_task_trace(M, torch_mod):
     for _ in range(4):
         M.asyncmap_(pool, s, rb, torch.zeros(n, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), comm, nwait=n)
     tr = comm.trace()
-    assert tr.shape == (4 * n, 10)
+    assert tr.shape == (4 * n, 11)
     F = {k: j for j, k in enumerate(M.DeviceComm.TRACE_FIELDS)}
     slack = 100_000  # ns: the device clock's calibration
     for e in tr:
