@@ -116,7 +116,8 @@ def replay(M, sc, comm, buf, host, predicate, snap=None):
         out.append({"repochs": pool.repochs.tolist(), "sepochs": pool.sepochs.tolist(),
                     "active": pool.active.astype(int).tolist(), "epoch": int(pool.epoch),
                     "latency_s": pool.latency.tolist(), "recv": snap(recv), "call_ms": call_ms,
-                    "t_ns": (t0_ns, time.perf_counter_ns()), "ranks": list(ranks)})
+                    "t_ns": (t0_ns, time.perf_counter_ns()), "ranks": list(ranks),
+                    "stimestamps": pool.stimestamps.tolist()})
     for r in out:
         r["recv"] = np.asarray(host(r["recv"])).tolist()
     return out, pool
@@ -192,6 +193,77 @@ def task_parts(e):
     return p
 
 
+def hop_check(sc, got, trace, task_tol=1e-3, obs_tol=1e-3, lat_tol=50e-6):
+    """Per-hop latency fidelity of a gated device replay against the oracle (tests/test_gpu_gated.py).
+
+    The device's latency of a harvest, like the reference's, is (harvest time) - (dispatch time)
+    (src/MPIAsyncPools.jl:105,164,215).  Its distance to the oracle's is the difference of two
+    drifts of the device timeline against the virtual clock -- at the dispatch and at the
+    harvest -- and those drifts accumulate along DIFFERENT chains: a re-dispatch inside the wait
+    loop (:177-184) runs on its worker's own chain of completions, a call's posts on the
+    coordinator's chain (the oracle's coordinator takes no time).  gpu_sep_nwait2's final
+    Waitall! harvests worker 1 at worker 4's completion: -1.3 ms against the oracle at every run
+    on the device (-3.4 ms over the HOST transport on CPU, where each hop costs more) with every
+    task and every observation on time (round 4's "residual miss", round 5's task trace).  So
+    the check is per hop, on the device's own clock (the task trace, mpa_comm_trace), for every
+    harvested task:
+
+      * latency semantics: pool.latency = trace harvest - trace post (within lat_tol);
+      * the task: its completion store - (its dispatch + its schedule duration)  (task_tol)
+        -- the injected straggler delay IS the schedule;
+      * the harvest: its time - the device time of the event the oracle harvested it at
+        (obs_tol): the completion store of the task(s) whose virtual completion is the
+        oracle's observation time, or, where none is (a phase-1 Test! at the call's start),
+        the call's start.
+
+    Every traced task the device harvested is matched to the oracle's event of the same worker
+    and task number (no matching by latency value: one worker's tasks can share a latency), and
+    the op that harvested it is the call whose host-time window holds its harvest.
+
+    Returns (misses, stats): misses are (kind, op, pool position, ms, tolerance ms); stats the
+    p50 / max of each hop in ms."""
+    mg = make_golden()
+    _, sim = mg.run_scenario(sc, return_sim=True)
+    events, done_at = {}, {}
+    for w, t, post, d, seen in sim.events():
+        events[(w, t)] = (post, d, seen)
+        done_at.setdefault(d, []).append((w, t))
+    n = sc["n"]
+    ranks = list(sc.get("ranks", list(range(1, n + 1))))
+    pos_of = {r: i for i, r in enumerate(ranks)}
+    tr = {(int(e[F["rank"]]), int(e[F["seq"]])): e for e in trace}
+    starts = np.asarray([g["t_ns"][0] for g in got], dtype=np.int64)
+    bad = []
+    hops = {"latency": [], "task": [], "harvest": []}
+    for (rank, t), e in sorted(tr.items()):
+        if not e[F["harvest"]] or rank not in pos_of or (pos_of[rank], t) not in events:
+            continue  # never harvested (still in flight at the end), or another pool's
+        i = pos_of[rank]
+        post, d, seen = events[(i, t)]
+        k = int(np.searchsorted(starts, e[F["harvest"]], side="right")) - 1  # the call that harvested it
+        if not e[F["pub"]] or k < 0:
+            bad.append(("untraced", k, i, None, None))
+            continue
+        lat_dev = got[k]["latency_s"][i] - (e[F["harvest"]] - e[F["post"]]) / 1e9
+        task_dev = (e[F["pub"]] - e[F["post"]] - (d - post)) / 1e9
+        trig = [tr.get((ranks[w2], t2)) for w2, t2 in done_at.get(seen, [])]
+        trig = [x[F["pub"]] for x in trig if x is not None and x[F["pub"]]]
+        t_trig = max(trig) if trig else got[k]["t_ns"][0]
+        obs_dev = (e[F["harvest"]] - t_trig) / 1e9
+        hops["latency"].append(lat_dev)
+        hops["task"].append(task_dev)
+        hops["harvest"].append(obs_dev)
+        if abs(lat_dev) > lat_tol:
+            bad.append(("latency", k, i, round(lat_dev * 1e3, 3), lat_tol * 1e3))
+        if abs(task_dev) > task_tol:
+            bad.append(("task", k, i, round(task_dev * 1e3, 3), task_tol * 1e3))
+        if obs_dev > obs_tol or obs_dev < -0.1e-3:
+            bad.append(("harvest", k, i, round(obs_dev * 1e3, 3), obs_tol * 1e3))
+    stats = {key: (round(float(np.median(v)) * 1e3, 3), round(float(np.max(np.abs(v))) * 1e3, 3))
+             for key, v in hops.items() if v}
+    return sorted(bad, key=lambda b: (b[1], b[2])), stats
+
+
 def explain_misses(got, trace, bad):
     """For each missed harvest (op k, pool position i): the harvested task's split, and the
     latest task (completion store - due) the gate waited for during that call."""
@@ -218,38 +290,6 @@ def trace_stats(trace):
         if len(v):
             st[key] = (round(float(np.median(v)), 3), round(float(np.percentile(v, 99)), 3), round(float(v.max()), 3))
     return st
-
-
-def _child_replay(name, own_stream, q):
-    try:
-        import torch
-        import mpiasyncpools as M
-        torch.zeros(1, device="cuda")
-        warm_kernels(M, torch, 4)
-        sc = next(s for s in scenarios() if s["name"] == name)
-        comm_n = sc.get("comm_workers", sc["n"])
-        dur = np.asarray(sc["durations_ns"], dtype=np.int64).reshape(comm_n, -1)
-        q.put(("ok",) + kmap2_replay(M, sc, dur, own_stream))
-    except BaseException as e:  # report, do not hang the parent
-        q.put(("error", repr(e), {}))
-
-
-def kmap2_replay_in_child(name, own_stream=True, timeout=300):
-    """kmap2_replay of the golden scenario `name` in a fresh (spawned) process."""
-    import multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    p = ctx.Process(target=_child_replay, args=(name, own_stream, q))
-    p.start()
-    try:
-        status, got, counters = q.get(timeout=timeout)
-    finally:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
-    if status != "ok":
-        raise RuntimeError("replay of %s in a child process failed: %s" % (name, got))
-    return got, dict(counters, fresh_process=1)
 
 
 def random_scenario(seed):
