@@ -190,10 +190,11 @@ __device__ __forceinline__ f32x4 ld_wt(const f32x4* p) {
 #if MPA_MEASURE
 // In-kernel clock (measurement build only; MI355X_MICROARCH.md 'DVFS give-back' item 6): thread 0
 // of every workgroup stamps s_memtime (shader cycles) and s_memrealtime (100 MHz) once before and
-// once after its block loop; the last launch's stamps are read by lsqp4_clock_dump() (MPA_LSQP4_CLOCK=1,
+// once after its block loop, and its block count; the last launch of two or more tasks (the 7- and 8-task
+// launches of the c5 loop, not the 1-task release after it) is read by lsqp4_clock_dump() (MPA_LSQP4_CLOCK=1,
 // at comm teardown).  Nothing in the kernel reads them.
 constexpr int kClockSlots = 4096;
-__device__ unsigned long long g_lsqp4_clk[kClockSlots][4];
+__device__ unsigned long long g_lsqp4_clk[kClockSlots][5];
 #endif
 
 // FULL: every task of the batch has cols == 2048 and rows % 16 == 0 (BASELINE c5's shape):
@@ -642,12 +643,13 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     if (u + 1 < nb) step(u + 1, my1, bring[1], part[1]);
   }
 #if MPA_MEASURE
-  if (tid == 0 && bx < kClockSlots) {
+  if (tid == 0 && bx < kClockSlots && batch.ntasks >= 2) {
     const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
     g_lsqp4_clk[bx][0] = clk0;
     g_lsqp4_clk[bx][1] = rt0;
     g_lsqp4_clk[bx][2] = clk1;
     g_lsqp4_clk[bx][3] = rt1;
+    g_lsqp4_clk[bx][4] = (unsigned long long)nb;
   }
 #endif
 #undef MPA_VMCNT
@@ -732,19 +734,22 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
 
 #if MPA_MEASURE
 void lsqp4_clock_dump() {
-  static unsigned long long h[kClockSlots][4];
+  static unsigned long long h[kClockSlots][5];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_lsqp4_clk), sizeof(h)) != hipSuccess) return;
-  std::vector<double> ghz, us;
+  std::vector<double> ghz, us, cyc;
   for (int b = 0; b < kClockSlots; ++b)
-    if (h[b][3] > h[b][1] && h[b][2] > h[b][0]) {
+    if (h[b][3] > h[b][1] && h[b][2] > h[b][0] && h[b][4] > 0) {
       ghz.push_back(double(h[b][2] - h[b][0]) / double(h[b][3] - h[b][1]) * 0.1);  // 100 MHz realtime
       us.push_back(double(h[b][3] - h[b][1]) / 100.0);
+      cyc.push_back(double(h[b][2] - h[b][0]) / double(h[b][4]));
     }
   if (ghz.empty()) return;
   std::sort(ghz.begin(), ghz.end());
   std::sort(us.begin(), us.end());
-  std::fprintf(stderr, "lsqp4 clock: %zu workgroups, in-kernel clock median %.3f GHz (min %.3f, max %.3f), block loop median %.1f us\n",
-               ghz.size(), ghz[ghz.size() / 2], ghz.front(), ghz.back(), us[us.size() / 2]);
+  std::sort(cyc.begin(), cyc.end());
+  std::fprintf(stderr, "lsqp4 clock: %zu workgroups of the last multi-task launch, in-kernel clock median %.3f GHz "
+               "(min %.3f, max %.3f), block loop median %.1f us, %.0f shader cycles per 16-row block (median)\n",
+               ghz.size(), ghz[ghz.size() / 2], ghz.front(), ghz.back(), us[us.size() / 2], cyc[cyc.size() / 2]);
 }
 #endif
 

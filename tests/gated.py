@@ -235,6 +235,14 @@ def hop_check(sc, got, trace, task_tol=1e-3, obs_tol=1e-3, lat_tol=50e-6):
     starts = np.asarray([g["t_ns"][0] for g in got], dtype=np.int64)
     bad = []
     hops = {"latency": [], "task": [], "harvest": []}
+    # the call that harvested each task; a worker harvested twice in one call (a stale harvest,
+    # its re-dispatch and the fresh one, :161-184) shows the later latency after the call
+    last = {}
+    for (rank, t), e in tr.items():
+        if e[F["harvest"]] and rank in pos_of:
+            k = int(np.searchsorted(starts, e[F["harvest"]], side="right")) - 1
+            if k >= 0 and e[F["harvest"]] >= last.get((k, pos_of[rank]), (0, 0))[0]:
+                last[(k, pos_of[rank])] = (e[F["harvest"]], t)
     for (rank, t), e in sorted(tr.items()):
         if not e[F["harvest"]] or rank not in pos_of or (pos_of[rank], t) not in events:
             continue  # never harvested (still in flight at the end), or another pool's
@@ -244,7 +252,7 @@ def hop_check(sc, got, trace, task_tol=1e-3, obs_tol=1e-3, lat_tol=50e-6):
         if not e[F["pub"]] or k < 0:
             bad.append(("untraced", k, i, None, None))
             continue
-        lat_dev = got[k]["latency_s"][i] - (e[F["harvest"]] - e[F["post"]]) / 1e9
+        lat_dev = got[k]["latency_s"][i] - (e[F["harvest"]] - e[F["post"]]) / 1e9 if last[(k, i)][1] == t else 0.0
         task_dev = (e[F["pub"]] - e[F["post"]] - (d - post)) / 1e9
         trig = [tr.get((ranks[w2], t2)) for w2, t2 in done_at.get(seen, [])]
         trig = [x[F["pub"]] for x in trig if x is not None and x[F["pub"]]]
