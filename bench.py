@@ -661,6 +661,11 @@ def main():
     args = parse()
     cfg = dict(CONFIGS[args.config])
     cfg["config"] = args.config
+    if os.environ.get("MPA_BENCH_ROWS"):
+        # rehearsals only (the control path with shards so small that the exchange runs alone):
+        # the line says so in its workload and is never a BASELINE measurement
+        cfg["rows"] = int(os.environ["MPA_BENCH_ROWS"])
+        cfg["desc"] = "REHEARSAL (MPA_BENCH_ROWS=%d, not the BASELINE size): " % cfg["rows"] + cfg["desc"]
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
