@@ -364,9 +364,10 @@ void HipComm::timer_loop() {
       // spin with the lock released; a task deferred meanwhile with an earlier deadline moves
       // tfront_ below `due` and ends the spin (the loop then takes the new front), as does a stop
       lk.unlock();
+      // yielding: on a core it shares with the coordinator's wait, neither holds the other off
       while (mono_ns() < due && tfront_.load(std::memory_order_acquire) >= due &&
              !tstop_spin_.load(std::memory_order_acquire))
-        __builtin_ia32_pause();
+        std::this_thread::yield();
       lk.lock();
       continue;
     }

@@ -15,6 +15,7 @@ void HipComm::serve() {
     ~Disarm() { c->disarm_all(); }
   } disarm_guard{this};
   std::vector<int64_t> fresh;
+  PoliteSpin idle;  // the doorbell poll between tasks (hot for kHotSpinNs, then yielding)
   for (int64_t r = 1; r <= nworkers_; ++r)
     if (w_[size_t(r - 1)].here && server_path(r) && armable(r)) arm(r);
   for (uint64_t spins = 0;; ++spins) {
@@ -87,9 +88,12 @@ void HipComm::serve() {
       }
       if (timing_) reap_timing(false);
       launch_tasks(fresh, /*staged=*/true);
+      idle = PoliteSpin{};
     } else if (!progress) {
       if ((spins & 0xFFF) == 0xFFF) watchdog(t0, /*timeout=*/false);
-      __builtin_ia32_pause();
+      idle();
+    } else {
+      idle = PoliteSpin{};  // busy again: the next idle stretch starts hot
     }
   }
 }

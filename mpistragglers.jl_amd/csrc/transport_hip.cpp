@@ -281,11 +281,12 @@ int64_t HipComm::waitany(int64_t n, const int64_t* ranks, const uint8_t* live) {
     release_held();
   }
   const auto t0 = Clock::now();
+  PoliteSpin poll;
   for (uint64_t spins = 0;; ++spins) {
     for (int64_t i = 0; i < n; ++i)
       if (live[i] && done(ranks[i])) return i;
     if ((spins & 0xFFF) == 0xFFF) watchdog(t0);
-    __builtin_ia32_pause();
+    poll();
   }
 }
 
@@ -295,9 +296,10 @@ void HipComm::waitall(int64_t n, const int64_t* ranks, const uint8_t* live) {
   const auto t0 = Clock::now();
   for (int64_t i = 0; i < n; ++i) {
     if (!live[i]) continue;
+    PoliteSpin poll;
     for (uint64_t spins = 0; !done(ranks[i]); ++spins) {
       if ((spins & 0xFFF) == 0xFFF) watchdog(t0);
-      __builtin_ia32_pause();
+      poll();
     }
   }
 }

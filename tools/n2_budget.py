@@ -17,7 +17,8 @@ region (the last K dispatches of each process):
                                                 word, the queued task starts)
   door wait seen  end W(e) - end L0(e-1)
   remote task     end L1(e) - start L1(e)
-  done -> step    end L0(e) - end L1(e)       (rank 0's tail sees `done`, harvests, updates, rings)
+  done -> end     end L0(e) - end L1(e)       (rank 0's launch after the remote reply: on one GPU
+                                                its own seven tasks, which share the HBM, are longer)
   epoch           end L0(e) - end L0(e-1)
 """
 import argparse
@@ -65,21 +66,24 @@ def main():
     if len(pids) != 2 or any(q not in by_pid for q in pids):
         raise SystemExit(f"trace pids {sorted(k for k in by_pid if k)} do not contain the ranks {pids}")
     r0 = [r for r in sorted(by_pid[pids[0]]) if "lsq_grad_kernel" in r[2]][-(K + 1):]
-    r1 = [r for r in sorted(by_pid[pids[1]]) if "lsq_grad_kernel" in r[2]][-K:]
+    r1 = [r for r in sorted(by_pid[pids[1]]) if "lsq_grad_kernel" in r[2]]
     w1 = [r for r in sorted(by_pid[pids[1]]) if "door_wait_kernel" in r[2]]
-    out = {"epochs": len(r1), "rank0_launches": len(r0), "rank1_launches": len(r1), "rank1_door_waits": len(w1)}
+    out = {"epochs": len(r0) - 1, "rank1_door_waits": len(w1)}
     ring, seen, remote, step, epoch, local = [], [], [], [], [], []
-    for e in range(1, min(len(r0), len(r1) + 1)):
+    for e in range(1, len(r0)):
         prev_end = r0[e - 1][1]
-        s1, e1 = r1[e - 1][0], r1[e - 1][1]
-        if s1 < prev_end:
-            continue  # not this epoch's pairing (the remote task started before the ring)
+        # the remote task rung by launch e - 1's tail: the first rank-1 task to start after its end
+        # (10 us of slack for the two processes' clocks)
+        cand = [r for r in r1 if prev_end - 10_000 <= r[0] <= r0[e][1]]
+        if not cand:
+            continue
+        s1, e1 = cand[0][0], cand[0][1]
         ring.append(s1 - prev_end)
         remote.append(e1 - s1)
         step.append(r0[e][1] - e1)
         epoch.append(r0[e][1] - prev_end)
         local.append(r0[e][1] - r0[e][0])
-        ws = [w for w in w1 if prev_end <= w[1] <= s1 + 1000]
+        ws = [w for w in w1 if prev_end - 10_000 <= w[1] <= s1]
         if ws:
             seen.append(ws[-1][1] - prev_end)
     out.update({"ring_to_start_us": med(ring), "door_wait_sees_ring_us": med(seen), "remote_task_us": med(remote),
