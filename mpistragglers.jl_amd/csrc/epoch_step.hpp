@@ -32,6 +32,8 @@ template <typename T, int V>
 __device__ __forceinline__ EVec<T, V> eld(const T* p) {
   if constexpr (V * sizeof(T) == 16) {
     return __builtin_bit_cast(EVec<T, V>, *reinterpret_cast<const uint4*>(p));
+  } else if constexpr (V * sizeof(T) == 8 && V > 1) {
+    return __builtin_bit_cast(EVec<T, V>, *reinterpret_cast<const uint2*>(p));
   } else if constexpr (V * sizeof(T) == 32) {
     struct U2 {
       uint4 a, b;
@@ -49,6 +51,8 @@ template <typename T, int V>
 __device__ __forceinline__ void est(T* p, const EVec<T, V>& v) {
   if constexpr (V * sizeof(T) == 16) {
     *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, v);
+  } else if constexpr (V * sizeof(T) == 8 && V > 1) {
+    *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, v);
   } else if constexpr (V * sizeof(T) == 32) {
     struct U2 {
       uint4 a, b;
@@ -62,8 +66,8 @@ __device__ __forceinline__ void est(T* p, const EVec<T, V>& v) {
   }
 }
 
-// V bf16 message elements as ONE store / load: 16 B at V = 8, 8 B at V = 4 (epoch_width
-// guarantees the alignment), element stores otherwise.  A remote worker's message slot is
+// V bf16 message elements as ONE store / load: 16 B at V = 8, 8 B at V = 4, 4 B at V = 2
+// (epoch_width guarantees the alignment), element stores otherwise.  A remote worker's message slot is
 // fine-grained memory of another GPU: element stores reached it as 2-byte partial writes
 // (c5 at N = 2 moved 22 GB/s, at N = 8 2.3 GB/s).
 template <int V>
@@ -74,6 +78,8 @@ __device__ __forceinline__ void st_bf16(uint16_t* p, const H16<V> h) {
     *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, h);
   } else if constexpr (V == 4) {
     *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, h);
+  } else if constexpr (V == 2) {
+    *reinterpret_cast<unsigned*>(p) = __builtin_bit_cast(unsigned, h);
   } else {
 #pragma unroll
     for (int e = 0; e < V; ++e) p[e] = h.v[e];
@@ -85,6 +91,8 @@ __device__ __forceinline__ H16<V> ld_bf16(const uint16_t* p) {
     return __builtin_bit_cast(H16<V>, *reinterpret_cast<const uint4*>(p));
   } else if constexpr (V == 4) {
     return __builtin_bit_cast(H16<V>, *reinterpret_cast<const uint2*>(p));
+  } else if constexpr (V == 2) {
+    return __builtin_bit_cast(H16<V>, *reinterpret_cast<const unsigned*>(p));
   } else {
     H16<V> h;
 #pragma unroll

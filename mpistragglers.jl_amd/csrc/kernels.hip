@@ -332,8 +332,24 @@ hipError_t launch_aggregate(int dtype, const AggregateArgs& a, hipStream_t s) {
 
 // Elements per thread of the epoch step: 16-B vectors of the iterate (4 fp32 / 2 fp64) when
 // the element count and every pointer the kernel touches allow it; fp32 with bf16 messages
-// (the batched variant) takes 8, so each message store is one 16-B vector (4: 8 B).
+// (the batched variant) up to 8, so each message store is one 16-B vector (4: 8 B).  A large
+// step (c5: 131072 elements) then narrows its vectors until the grid covers the chip
+// (kEpochMinGrid workgroups, one per CU), down to 8-B accesses: at 8 elements per thread c5's
+// step ran on 64 workgroups.
+#ifndef MPA_EPOCH_MIN_GRID
+#define MPA_EPOCH_MIN_GRID 256
+#endif
+static int epoch_width_max(int dtype, const EpochArgs& a);
 int epoch_width(int dtype, const EpochArgs& a) {
+  int v = epoch_width_max(dtype, a);
+  const int floor_v = dtype == MPA_F64 ? 1 : 2;  // keep 8-B accesses
+  // (a small step -- c1-c4's iterate of 64-2048 elements -- keeps its widest vectors: one or a
+  // few workgroups either way)
+  while (v > floor_v && a.elems / v / kThreads < MPA_EPOCH_MIN_GRID && a.elems / v / kThreads >= 32) v /= 2;
+  return v;
+}
+
+static int epoch_width_max(int dtype, const EpochArgs& a) {
   uintptr_t m = reinterpret_cast<uintptr_t>(a.recv) | reinterpret_cast<uintptr_t>(a.x);
   for (int i = 0; i < a.n; ++i)
     m |= reinterpret_cast<uintptr_t>(a.hsrc[i]) | reinterpret_cast<uintptr_t>(a.hsrc2[i]);
@@ -345,7 +361,7 @@ int epoch_width(int dtype, const EpochArgs& a) {
   return a.elems % 4 == 0 && (m & 15u) == 0 && (mb & 7u) == 0 ? 4 : 1;
 }
 
-bool epoch_vec(int dtype, const EpochArgs& a) { return epoch_width(dtype, a) > 1; }
+bool epoch_vec(int dtype, const EpochArgs& a) { return epoch_width_max(dtype, a) > 1; }
 
 int epoch_grid(int dtype, const EpochArgs& a) {
   const int V = epoch_width(dtype, a);
@@ -359,7 +375,8 @@ hipError_t launch_epoch(int dtype, const EpochArgs& a, hipStream_t s) {
   const bool vec = width > 1;
   if (dtype == MPA_F32) {
     if (width == 8) hipLaunchKernelGGL((epoch_kernel<float, 8>), dim3(grid), dim3(kThreads), 0, s, a);
-    else if (vec) hipLaunchKernelGGL((epoch_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, s, a);
+    else if (width == 4) hipLaunchKernelGGL((epoch_kernel<float, 4>), dim3(grid), dim3(kThreads), 0, s, a);
+    else if (width == 2) hipLaunchKernelGGL((epoch_kernel<float, 2>), dim3(grid), dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL((epoch_kernel<float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   } else if (dtype == MPA_F64) {
     if (vec) hipLaunchKernelGGL((epoch_kernel<double, 2>), dim3(grid), dim3(kThreads), 0, s, a);
