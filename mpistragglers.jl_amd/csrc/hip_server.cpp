@@ -115,7 +115,7 @@ bool HipComm::armable(int64_t rank) const {
   int here = 0;
   for (const auto& v : w_) here += v.here;
   if (here != 1) return false;
-  return arm_wave_ || w.box->coord_dev != dev_;
+  return arm_wave_ || w.box->coord_dev != dev_ || arm_force_;
 }
 
 // The worker's next task is launched before rank 0 posts it and waits for the worker's device

@@ -853,6 +853,7 @@ class HipComm final : public Comm {
   bool debug_ = false;
   int arm_mode_ = 0;
   bool arm_wave_ = true;  // MPA_ARM_WAIT: an armed task waits behind a one-wave door_wait_kernel
+  bool arm_force_ = false;  // MPA_ARM_WAIT_FORCE=1 (measurement build): in-kernel waits on rank 0's GPU too
   bool batch_gather_ = true;  // MPA_GATHER=0: a server launches whatever one doorbell scan found
   // undelayed task batches run on the coordinator stream behind the exchange that delivered
   // their messages (MPA_COORD_BATCH=0: on a launch stream behind a cross-queue event wait,

@@ -126,6 +126,10 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   // how an armed task waits: one wave ahead of it (default) or every workgroup in-kernel
   const char* aw = std::getenv("MPA_ARM_WAIT");
   arm_wave_ = !(aw && !std::strcmp(aw, "kernel"));
+  // measurement build: the in-kernel wait also on a GPU rank 0 uses (the one-GPU rehearsal of
+  // the node's path; the product refuses it there)
+  const char* af = measure_env("MPA_ARM_WAIT_FORCE");
+  arm_force_ = af && *af == '1';
   const char* cb = measure_env("MPA_COORD_BATCH");
   coord_batches_ = !(cb && *cb == '0');
   fused_tail_ = !env_off("MPA_TAIL");

@@ -51,6 +51,35 @@ __global__ void __launch_bounds__(256) store_kernel(const float* __restrict__ x,
   }
 }
 
+// the step's reply gather: kDst chunks of kElems fp32 read with 16-B loads, summed per element
+__global__ void __launch_bounds__(256) gather_kernel(Dsts src, float* __restrict__ out) {
+  const int j = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (j >= kElems) return;  // each chunk holds kElems fp32 = 512 KiB
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int d = 0; d < kDst; ++d) {
+    const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src.d[d]) + j);
+    s.x += v.x, s.y += v.y, s.z += v.z, s.w += v.w;
+  }
+  *reinterpret_cast<float4*>(out + j) = s;
+}
+
+static double run_gather(const Dsts& d, float* out, hipStream_t s, int reps) {
+  const int grid = (kElems / 4 + 255) / 256;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int r = 0; r < 10; ++r) hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(256), 0, s, d, out);
+  CK(hipEventRecord(a, s));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(256), 0, s, d, out);
+  CK(hipEventRecord(b, s));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return double(ms) * 1e3 / reps;
+}
+
 template <int W, int MODE>
 static double run(const float* x, const Dsts& d, hipStream_t s, int reps) {
   const int grid = (kElems / W + 255) / 256;
@@ -87,6 +116,20 @@ int main() {
     std::printf("%-15s 2-B element stores %7.2f us (%6.1f GB/s) | 8-B vectors %7.2f us (%6.1f GB/s) | 16-B vectors %7.2f us (%6.1f GB/s)\n",
                 kind, t0, bytes / t0 / 1e3, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3);
     for (int k = 0; k < kDst; ++k) CK(hipFree(d.d[k]));
+    // the reply gather: 7 chunks of 512 KiB fp32 (c5's reply per worker) read from this kind of memory
+    Dsts g;
+    for (int k = 0; k < kDst; ++k) {
+      if (fine) CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&g.d[k]), kElems * 4, hipDeviceMallocFinegrained));
+      else CK(hipMalloc(&g.d[k], kElems * 4));
+      CK(hipMemset(g.d[k], 0, kElems * 4));
+    }
+    float* out;
+    CK(hipMalloc(&out, kElems * 4));
+    const double tg = run_gather(g, out, s, 200);
+    std::printf("%-15s reply gather (7 x 512 KiB fp32, 16-B loads) %7.2f us (%6.1f GB/s read)\n", kind, tg,
+                double(kDst) * kElems * 4 / tg / 1e3);
+    for (int k = 0; k < kDst; ++k) CK(hipFree(g.d[k]));
+    CK(hipFree(out));
   }
   CK(hipFree(x));
   return 0;
