@@ -545,3 +545,79 @@ def lsq_sched_dist(rank, world, port, placement, config, epoch0, result_q):
     except Exception:
         result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
         raise
+
+
+def armed_timeout_dist(rank, world, port, result_q):
+    """A device-armed task whose doorbell never comes: rank 1 serves one least-squares
+    worker, armed behind a one-wave doorbell wait bounded at MPA_WAIT_TIMEOUT_S = 2 s; rank 0 posts
+    it once (the path is decided, the task runs, the server arms the next one) and then never again.
+    The wait must time out, cancel the queued task -- which then neither writes its reply nor
+    publishes `done` -- and report the device error: rank 1's serve() raises it, and the worker's
+    task count stays at 1."""
+    import time
+    import numpy as np
+    try:
+        if rank == 1:
+            os.environ["MPA_WAIT_TIMEOUT_S"] = "2"
+        os.environ.pop("MPA_ARM", None)
+        dist = _init(rank, world, port)
+        import torch
+        torch.cuda.set_device(0)
+        import mpiasyncpools as M
+        n, rows, cols = 1, 512, 256
+        name = [f"/mpa_to{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+        if rank == 0:
+            comm = M.DistComm(n, [1], 0, name[0], cols * 4, transport="hip")
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            comm = M.DistComm(n, [1], rank, name[0], cols * 4, transport="hip")
+            A = torch.empty(rows, cols, device="cuda")
+            b = torch.empty(rows, device="cuda")
+            M.generate(A, 3, 0, 0, float(np.float32(1 / np.sqrt(cols))))
+            M.generate(b, 3, 1, 0, 1.0)
+            comm.set_task_lsq(1, A, b)
+            torch.cuda.synchronize()
+        dist.barrier()
+        if rank != 0:
+            t0 = time.perf_counter()
+            err = None
+            try:
+                comm.serve()
+            except Exception as e:  # the expected outcome
+                err = str(e)
+            msg = [(err, round(time.perf_counter() - t0, 2), comm.counter("armed"))]
+            dist.broadcast_object_list(msg, src=1)
+            dist.barrier()
+            comm.close()
+            dist.destroy_process_group()
+            return
+        pool = M.MPIAsyncPool(n)
+        x = torch.zeros(cols, device="cuda")
+        recv = torch.zeros(cols, device="cuda")
+        M.asyncmap_(pool, x, recv, torch.zeros(cols, device="cuda"), torch.zeros_like(recv), comm, nwait=1)
+        errors = []
+        if comm.tasks_done(1) != 1:
+            errors.append(("first task", comm.tasks_done(1)))
+        msg = [None]
+        dist.broadcast_object_list(msg, src=1)  # rank 1's serve() returned (or raised)
+        err, waited, armed = msg[0]
+        if not err or "in-kernel wait timed out" not in err:
+            errors.append(("serve() did not report the timed-out wait", err))
+        if not (1.5 <= waited <= 60):
+            errors.append(("serve() ended after", waited))
+        if armed < 2:
+            errors.append(("armed launches", armed))
+        time.sleep(0.5)
+        if comm.tasks_done(1) != 1:  # the cancelled task published nothing
+            errors.append(("the timed-out task published", comm.tasks_done(1)))
+        try:
+            comm.shutdown()
+        except Exception:
+            pass  # the shared error word is set: rank 0's own wait may report it too
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        result_q.put(("ok", errors))
+    except Exception:
+        result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
+        raise

@@ -132,3 +132,13 @@ def test_sched_eight_processes(built, config, epoch0):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run(dist_worker.lsq_sched_dist, 8, list(range(8)), config, epoch0, timeout=240)
+
+
+def test_armed_wait_timeout_cancels_the_task(built):
+    """a device-armed task whose doorbell wait times out is cancelled (the one-wave
+    door_wait_kernel stores the task's seq into its go word): no reply, no `done`, the error
+    reported by the server's serve()."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(dist_worker.armed_timeout_dist, 2, timeout=120)
