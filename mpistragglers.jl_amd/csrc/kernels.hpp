@@ -281,6 +281,10 @@ hipError_t launch_lsqp5(const LsqpBatch& a, hipStream_t s);
 // (measure/lsqp6_kernel.hip, measurement build: MPA_LSQP6=1; bitwise equal to lsqp4, 23 % faster
 // with L2-hot loads, equal streaming A from HBM: DESIGN.md §10)
 hipError_t launch_lsqp6(const LsqpBatch& a, hipStream_t s);
+// lsqp4 by pairs of 16-row blocks: phase 2 over the pair's 32 distinct rows, hi and lo as two
+// MFMAs, half the transposed LDS reads (measure/lsqp7_kernel.hip, measurement build: MPA_LSQP7=1;
+// FULL batches, others go to lsqp4)
+hipError_t launch_lsqp7(const LsqpBatch& a, hipStream_t s);
 // Single pass by COLUMN pairs (lsqc_kernel.hip): the two members of a row group split the
 // columns (member h: columns 1024 h .. 1024 h + 1023), each holding all 64 iterates of its G
 // columns, and exchange their 16 x 64 partial products per 16-row block as tagged granules.

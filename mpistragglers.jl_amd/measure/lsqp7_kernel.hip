@@ -1,0 +1,650 @@
+// lsqp4 by PAIRS of 16-row blocks (BASELINE configs[4], "c5"; measurement build, MPA_LSQP7=1):
+//     G_i = A_i^T (A_i X - B_i)      A_i rows x cols bf16, X cols x 64 bf16, B_i rows x 64 bf16
+// lsqp4_kernel.hip's cut (pairs of workgroups on one XCD by iterate halves, 4 waves of 512
+// registers, a private 2-slot strip ring per wave, phase 1 split-K over the waves) with one
+// change in phase 2.  lsqp4's phase-2 MFMA (K = 32) multiplies rows 0-15 of ONE block twice --
+// k 0-15 the hi residual, k 16-31 the lo residual -- so its B operand reads every A element twice
+// from LDS (lanes 32-63 hold a copy of lanes 0-31's operand; the MFMA's lane-group broadcast does
+// not exist for this instruction on gfx950, tools/probe_blgp.hip).  Here a step takes TWO blocks
+// (the ring's two slots): phase 1 of block u, phase 1 of block u + 1, their partials, ONE reduce,
+// and phase 2 as K = 32 over the pair's 32 DISTINCT rows (k 0-15 block u, k 16-31 block u + 1,
+// lanes 32-63 reading the other slot), once with the hi residual and once with the lo: the same
+// MFMAs, half the transposed LDS reads.  The pair's residual images come from the same two lane
+// swaps as lsqp4's (hi_u | hi_u+1 and lo_u | lo_u+1 instead of hi | lo).  The next pair's strips
+// refill both slots as phase 2 frees them (lead: the rest of phase 2 plus phase 1 of the blocks
+// before; the L2 prefetch pfd blocks ahead keeps those DMAs L2 hits).  FULL batches only (every
+// task 2048 columns, rows % 16 == 0; launch_lsqp7 hands other batches to lsqp4).  The sums are
+// regrouped (hi and lo of a pair in two MFMAs), so G agrees with lsqp4 to rounding, not bitwise.
+//
+// MFMA maps (cdna_hip_programming.md §3), 16x16x32 bf16: A[m=i][k=8g+j], B[k=8g+j][n=i],
+// C/D[m=4g+r][n=i]; lane l: i = l & 15, g = l >> 4.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "mpiasyncpools.h"
+
+
+namespace mpa {
+namespace {
+
+using namespace dev;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int K = kLsqbIterates;      // 64 iterates
+constexpr int QW = 4;                 // waves per workgroup, one per SIMD
+constexpr int QT = QW * 64;           // threads
+constexpr int PRB = 16;               // rows per block
+constexpr int QKW = 512;              // columns per wave
+constexpr int ROWB = QKW * 2;         // bytes of one slice row (1 KiB)
+constexpr int NKS = QKW / 32;         // k-steps of phase 1 (16)
+constexpr int NCT = QKW / 16;         // column tiles of phase 2 (32)
+constexpr int PH = 32;                // iterates per workgroup (one half)
+constexpr int SLICE = PRB * ROWB;     // 16 KiB
+constexpr int XS = PH * 2 + 16;       // X staging row stride (bytes)
+constexpr int PF = 4;                 // G tree fan-in
+#ifndef MPA_LSQP4_P2L
+#define MPA_LSQP4_P2L 1               // phase-2 transposed-read chunks in flight ahead (1 vs 2: -1 %, r02_c5_strip_ring.txt)
+#endif
+#ifndef MPA_LSQP4_AD
+#define MPA_LSQP4_AD 3                // phase-1 fragment read-ahead in k-steps (3 beats 2, 4, 6)
+#endif
+static_assert(QW * QKW == kLsqpMaxCols, "4 waves x 512 columns");
+static_assert(NKS == 16 && NCT == 32, "8 strips of 64 columns per wave");
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// Phase 1's accumulators in VGPRs.  G takes all 256 AGPRs, and the compiler gives every MFMA
+// intrinsic AGPR accumulators, so with intrinsics it parks 8 G registers in VGPRs around every
+// phase 1 (24 moves per block).  These asm forms keep the phase-1 chain in VGPRs.  Hazards are
+// the kernel's (the compiler does not look inside): the chain reads its own previous result as
+// SrcC (exact overlap: back to back is allowed), A / B operands come from LDS reads (lgkmcnt,
+// which the compiler does insert for asm operands) or registers written long before; the one
+// non-MFMA reader of the result gets 16 wait states first (mfma_v_settle)
+__device__ __forceinline__ f32x4 mfma_v0(const bf16x8& a, const bf16x8& b) {
+  f32x4 d;
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ void mfma_v(f32x4& d, const bf16x8& a, const bf16x8& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_v_settle(f32x4& d0, f32x4& d1) {
+  asm volatile("s_nop 7\n\ts_nop 7" : "+v"(d0), "+v"(d1));
+}
+__device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xc07f); }  // lgkmcnt(0)
+// lgkmcnt(N) alone (vmcnt / expcnt fields left free)
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  static_assert(N >= 0 && N < 16, "lgkmcnt is 4 bits");
+  __builtin_amdgcn_s_waitcnt(0xc07f | (N << 8));
+}
+// workgroup barrier that leaves the vector-memory queue alone (the next block's DMA stays in
+// flight): LDS traffic drained, then s_barrier; the clobber pins LDS accesses on either side
+__device__ __forceinline__ void barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS-DMA of one 1-KiB slice row: lane l's 16 B land at lds + 16 l.  Scalar base + 32-bit lane
+// offset (the saddr form).  Inline asm on purpose, as in lsqp_kernel.hip: the compiler would
+// guard every LDS read that may alias a DMA it knows of with vmcnt(0), waiting for the NEXT
+// block too; the kernel orders its reads itself (vmcnt per block).
+__device__ __forceinline__ void dma_row(const void* sbase, uint32_t voff, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l) : "memory");
+}
+__device__ __forceinline__ void pf4(const void* src, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(l) : "memory");
+}
+__device__ __forceinline__ void dma16(const void* src, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(l) : "memory");
+}
+// the saddr forms with an immediate offset (FULL blocks): the instruction adds OFF to the
+// global address AND to the LDS address (llvm.amdgcn.global.load.lds: "applied to both"), so
+// m0 = LDS destination - OFF.  One scalar base per block instead of a 64-bit add per strip
+// A whole strip (both halves) under one M0 write: half j lands at lds + 1024 j and reads its
+// rows at voff_j, so with m0 = lds - OFF and offsets OFF and OFF + 1024 the second half's lane
+// offset is passed as voff_1 - 1024 (voff_1 >= 8 rows >= 1024 B)
+template <int OFF>
+__device__ __forceinline__ void dma_strip_off(const void* sbase, uint32_t voff0, uint32_t voff1m, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds))) - uint32_t(OFF);
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2 offset:%4\n\t"
+               "global_load_lds_dwordx4 %1, %2 offset:%5"
+               ::"v"(voff0), "v"(voff1m), "s"(sbase), "s"(l), "i"(OFF), "i"(OFF + 1024) : "memory");
+}
+__device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l) : "memory");
+}
+__device__ __forceinline__ void pf4_s(const void* sbase, uint32_t voff, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds)));
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(l) : "memory");
+}
+
+// 16-B chunk c of strip row r sits at chunk position c ^ sw(r) (bits 1-2 only: chunk pairs
+// stay together); found by search over the linear maps of r's bits for conflict-free reads of
+// both phases (tools/lsqp4_swizzle.py)
+__host__ __device__ constexpr int sw(int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); }
+
+// write-through 16-B store / load as two 8-B agent-scope accesses (the G tree's hand-off:
+// MI355X_MICROARCH.md §inter-workgroup visibility, "one lane adds for the producer, the last
+// adder loads")
+__device__ __forceinline__ void st_wt(f32x4* p, const f32x4& v) {
+  const unsigned long long* s = reinterpret_cast<const unsigned long long*>(&v);
+  unsigned long long* d = reinterpret_cast<unsigned long long*>(p);
+  __hip_atomic_store(d, s[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(d + 1, s[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ f32x4 ld_wt(const f32x4* p) {
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+  unsigned long long u[2];
+  u[0] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  u[1] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_bit_cast(f32x4, u);
+}
+
+
+// FULL: every task of the batch has cols == 2048 and rows % 16 == 0 (BASELINE c5's shape):
+// no ragged block, no partial strip, so the block loop drops the clamps, selects and masks
+// of the general form and addresses a block from ONE scalar base (immediate strip offsets)
+template <bool ARMED>
+__global__ void __launch_bounds__(QT, 1) lsqp7_kernel(LsqpBatch batch) {
+  constexpr bool FULL = true;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[QW][2][SLICE];
+  __shared__ __attribute__((aligned(16))) uint8_t bring[2][PRB * PH * 2];
+  // phase-1 partials of the pair's two blocks (one buffer: a second barrier after the reduce reads)
+  __shared__ __attribute__((aligned(16))) f32x4 part[QW][2][2][64];
+  __shared__ __attribute__((aligned(16))) uint32_t sink[QW][64];
+  // zeros in B's slot layout, one per wave (each wave zeroes its own: no barrier): the -B MFMA
+  // operand of waves 1-3
+  __shared__ __attribute__((aligned(16))) uint8_t bzero[QW][PRB * PH * 2];
+
+  // blocks b and b + 8 are the two halves of one pair (one XCD under round-robin placement;
+  // speed only): pair index = (b / 16) * 8 + b % 8
+  const int bx = int(blockIdx.x);
+  const int h = (bx >> 3) & 1;
+  const int pidx = (bx >> 4) * 8 + (bx & 7);
+  if (pidx >= batch.grp0[batch.ntasks]) return;  // grid padding (whole workgroup)
+  int ti = 0;
+  while (ti + 1 < batch.ntasks && pidx >= batch.grp0[ti + 1]) ++ti;
+  const LsqpTask& a = batch.t[ti];
+  // a pre-armed task its server cancelled computes but neither writes G nor publishes: the
+  // go word (host memory) is read once per writing wave at the end (disarmed() below), not by
+  // every workgroup before any work (profiles/r02_arm_go_word.txt)
+  const int q = pidx - batch.grp0[ti];
+  const int ng = batch.grp0[ti + 1] - batch.grp0[ti];
+  if constexpr (ARMED)
+    if (!wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed
+
+  const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  const int qq = (lane >> 2) & 3, p4 = lane & 3;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t rows = a.rows;
+  const int cols = a.cols;
+  const int c0 = w * QKW;
+  // valid k-steps of this wave; the loops always run all of them (k-steps past cols meet
+  // X = 0, their G columns are never stored): branch-free block loop
+  const int nks = cols > c0 ? ((cols - c0) < QKW ? (cols - c0) : QKW) / 32 : 0;
+  const int64_t nblocks = (rows + PRB - 1) / PRB;
+  // wave-uniform by construction; readfirstlane keeps the block arithmetic on the scalar unit
+  // block indices in 32 bits (SALU has no 64-bit compare): the clamps below stay scalar
+  const int kb0 = __builtin_amdgcn_readfirstlane(int(nblocks * q / ng)),
+            kb1 = __builtin_amdgcn_readfirstlane(int(nblocks * (q + 1) / ng));
+  const int kblast = kb1 > kb0 ? kb1 - 1 : kb0;  // past the range, DMAs re-read this block
+  const int nb = int(kb1 - kb0);
+  const uint16_t* __restrict__ A = static_cast<const uint16_t*>(a.A);
+  const uint16_t* __restrict__ Bm = static_cast<const uint16_t*>(a.B);
+  const uint8_t* __restrict__ X = static_cast<const uint8_t*>(a.X);
+  uint8_t* my0 = &ring[w][0][0];
+  uint8_t* my1 = &ring[w][1][0];
+
+  // ---- X_h slice -> XF, through the wave's two ring slots (32 KiB) in two rounds of eight
+  // k-steps (32 X rows x 64 B each, row stride XS)
+  bf16x8 XF[NKS][2];
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd) {
+    uint4 xr[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int s = 8 * rd + (e >> 1), piece = lane + 64 * (e & 1), r = piece >> 2, c16 = piece & 3;
+      xr[e] = s < nks ? *reinterpret_cast<const uint4*>(X + (size_t(c0 + 32 * s + r) * K + PH * h) * 2 + c16 * 16)
+                      : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int piece = lane + 64 * (e & 1), r = piece >> 2, c16 = piece & 3;
+      *reinterpret_cast<uint4*>(my0 + ((e >> 1) * 32 + r) * XS + c16 * 16) = xr[e];
+    }
+    lgkm_drain();
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        // rows 8g + qq (elements 0-3) and 8g + 4 + qq (4-7), iterate columns 16t + 4p4 .. +3
+        const uint8_t* a0 = my0 + (s * 32 + 8 * g + qq) * XS + 2 * (16 * t) + 8 * p4;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * XS));
+        XF[8 * rd + s][t] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    lgkm_drain();
+  }
+  *reinterpret_cast<uint4*>(&bzero[w][16 * lane]) = make_uint4(0, 0, 0, 0);
+  lgkm_drain();
+
+  // ---- the wave's DMA of block kb (clamped: past the range it re-reads the range's last
+  // block into the free slot, unused, so every step issues the same number of loads)
+  const int64_t lda = a.lda;
+  // ---- the strip ring.  A wave's slice of a block (16 rows x 512 columns) is 8 strips of 64
+  // columns; strip k (2 KiB) sits at k * 2048, row r of it (128 B) at r * 128, logical 16-B
+  // chunk c of the row at position c ^ sw(r): bank-conflict free for phase 1's row reads and
+  // phase 2's transposed reads.  One DMA instruction moves half a strip (8 rows x 128 B; lane l:
+  // row 8j + l / 8, position l % 8), so phase 2 hands a strip back as soon as its four column
+  // tiles are read, and phase 1 waits for a block strip by strip.
+  // Per-lane offsets from the block's first row at column c0: strip half j, a full strip or
+  // one whose last 32 columns lie past cols (cols % 32 == 0; those lanes re-read the first 32)
+  uint32_t vfull[2], vpart[2];
+  auto voffs = [&](int nv, uint32_t (&vf)[2], uint32_t (&vp)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pr = 8 * j + (lane >> 3);     // row position in the strip
+      const int rr = pr < nv ? pr : nv - 1;   // rows past the end re-read the last row (R = 0)
+      const int c = (lane & 7) ^ sw(pr);
+      const uint32_t rb = uint32_t(rr) * uint32_t(lda) * 2u;
+      vf[j] = rb + uint32_t(c) * 16u;
+      vp[j] = rb + uint32_t(c & 3) * 16u;
+    }
+  };
+  voffs(PRB, vfull, vpart);
+  struct Blk {
+    const uint16_t* p;  // first row of the block (clamped into the range)
+    int nv;             // valid rows
+  };
+  auto blk = [&](int kb) __attribute__((always_inline)) {
+    const int kc = kb < kb1 ? kb : kblast;
+    const int64_t r0 = int64_t(kc) * PRB;
+    return Blk{A + r0 * lda, int(rows - r0 < PRB ? rows - r0 : PRB)};
+  };
+  // strip k of a block into a slot: 2 instructions.  Strips wholly past cols load columns
+  // 0 .. 31 (finite data that meets X = 0; their G columns are never stored)
+  auto dma_strip = [&](const Blk& b, const uint32_t (&vf)[2], const uint32_t (&vp)[2], int k, uint8_t* slot)
+      __attribute__((always_inline)) {
+    if constexpr (FULL) {
+      // every strip of every block lies inside the rows: base = the block's first row at c0,
+      // strip k at the immediate offset 128 k (k is a constant once the loops are unrolled)
+      const uint16_t* base = b.p + c0;
+      const uint32_t v1m = vf[1] - 1024u;
+      uint8_t* d = slot + 2048 * k;
+      switch (k) {
+        case 0: dma_strip_off<0>(base, vf[0], v1m, d); break;
+        case 1: dma_strip_off<128>(base, vf[0], v1m, d); break;
+        case 2: dma_strip_off<256>(base, vf[0], v1m, d); break;
+        case 3: dma_strip_off<384>(base, vf[0], v1m, d); break;
+        case 4: dma_strip_off<512>(base, vf[0], v1m, d); break;
+        case 5: dma_strip_off<640>(base, vf[0], v1m, d); break;
+        case 6: dma_strip_off<768>(base, vf[0], v1m, d); break;
+        default: dma_strip_off<896>(base, vf[0], v1m, d); break;
+      }
+    } else {
+      const int cb = c0 + 64 * k;
+      const bool full = cb + 64 <= cols;
+      const uint16_t* base = b.p + (cb < cols ? cb : 0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma_row(base, full ? vf[j] : vp[j], slot + 2048 * k + 1024 * j);
+    }
+  };
+  auto dma = [&](int kb, uint8_t* slot) __attribute__((always_inline)) {
+    const Blk b = blk(kb);
+    uint32_t vf[2], vp[2];
+    voffs(b.nv, vf, vp);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dma_strip(b, vf, vp, k, slot);
+  };
+  // L2 prefetch of block kb: 4 B per lane into a per-wave sink nobody reads, a lane per 128-B
+  // line; member h takes rows 8h .. 8h + 7 of the wave's slice (the pair shares the XCD's L2),
+  // so the DMA of the block, pfd steps later, finds its lines on chip.  Always issued (pfd = 0
+  // re-touches the block being loaded), so every wait counts the same loads
+  const int pfd = batch.pfd;
+  const uint32_t pfoff = uint32_t(c0 + 64 * (lane & 7) < cols ? c0 + 64 * (lane & 7) : 0) * 2u;
+  const uint32_t pfv = uint32_t(lane >> 3) * uint32_t(lda) * 2u + pfoff;  // FULL: lane offset from row 8h
+  auto pf = [&](int kb) __attribute__((always_inline)) {
+    const int kc = kb < kb1 ? kb : kblast;
+    if constexpr (FULL) {
+      pf4_s(A + (int64_t(kc) * PRB + 8 * h) * lda, pfv, &sink[w][0]);
+    } else {
+      int64_t row = int64_t(kc) * PRB + 8 * h + (lane >> 3);
+      row = row < rows ? row : rows - 1;
+      pf4(reinterpret_cast<const uint8_t*>(A + row * lda) + pfoff, &sink[w][0]);
+    }
+  };
+  // B of a block (16 rows x 32 iterates of half h = 16 x 64 B): one instruction of wave 0; the
+  // other waves touch the same rows into their sink instead, so every wave counts one load
+  const int brow = lane >> 2, bpiece = lane & 3;
+  const uint32_t bv = uint32_t(brow * K + 8 * bpiece) * 2u;  // FULL: lane offset from the block's first B row
+  auto dma_b = [&](int kb, uint8_t* bslot) __attribute__((always_inline)) {
+    const int kc = kb < kb1 ? kb : kblast;
+    if constexpr (FULL) {
+      const uint16_t* sb = Bm + int64_t(kc) * PRB * K + PH * h;
+      if (w == 0) dma16_s(sb, bv, bslot);
+      else pf4_s(sb, bv, &sink[w][0]);
+    } else {
+      int64_t row = int64_t(kc) * PRB + brow;
+      row = row < rows ? row : rows - 1;
+      const uint16_t* src = Bm + row * K + PH * h + 8 * bpiece;
+      if (w == 0) dma16(src, bslot);
+      else pf4(src, &sink[w][0]);
+    }
+  };
+  // vmcnt(n) alone (expcnt / lgkmcnt fields left free)
+#define MPA_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
+  // Issue order of a step (and of the prologue): B of the pair's two blocks, then per chunk c
+  // strip c of the first block and strip c of the second (2 instructions each), then the two
+  // prefetches.  Strip k of the current pair's first block has landed once at most the loads
+  // issued after it are pending: strip k of the second (2), the later chunks (4 each), the two
+  // prefetches; of the second block: the later chunks and the prefetches.  (The pair's phase 1
+  // runs before the step issues anything.)  k is a constant after unrolling: one wait survives.
+  auto wait_strip = [&](int b, int k) __attribute__((always_inline)) {
+    if (b == 0) {
+      switch (k) {
+        case 0: MPA_VMCNT(4 * 7 + 4); break;
+        case 1: MPA_VMCNT(4 * 6 + 4); break;
+        case 2: MPA_VMCNT(4 * 5 + 4); break;
+        case 3: MPA_VMCNT(4 * 4 + 4); break;
+        case 4: MPA_VMCNT(4 * 3 + 4); break;
+        case 5: MPA_VMCNT(4 * 2 + 4); break;
+        case 6: MPA_VMCNT(4 * 1 + 4); break;
+        default: MPA_VMCNT(4); break;
+      }
+    } else {
+      switch (k) {
+        case 0: MPA_VMCNT(4 * 7 + 2); break;
+        case 1: MPA_VMCNT(4 * 6 + 2); break;
+        case 2: MPA_VMCNT(4 * 5 + 2); break;
+        case 3: MPA_VMCNT(4 * 4 + 2); break;
+        case 4: MPA_VMCNT(4 * 3 + 2); break;
+        case 5: MPA_VMCNT(4 * 2 + 2); break;
+        case 6: MPA_VMCNT(4 * 1 + 2); break;
+        default: MPA_VMCNT(2); break;
+      }
+    }
+  };
+
+  f32x4 G[2][NCT];  // G^T tiles: [iterate tile][column tile], lane (i, g): its 4g + r, column i
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) G[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the pair (kb, kb + 1) into the two slots in the order wait_strip counts
+  auto issue_pair = [&](int kb) __attribute__((always_inline)) {
+    dma_b(kb, bring[0]);
+    dma_b(kb + 1, bring[1]);
+    const Blk b0 = blk(kb), b1 = blk(kb + 1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      dma_strip(b0, vfull, vpart, k, my0);
+      dma_strip(b1, vfull, vpart, k, my1);
+    }
+    pf(kb + pfd);
+    pf(kb + 1 + pfd);
+  };
+  for (int d = 2; d < pfd; ++d) pf(kb0 + d);
+  issue_pair(kb0);
+
+  // LDS offsets inside a slot: k-step s reads chunk 4 (s & 1) + g of row i of strip s / 2;
+  // column tile ct reads chunks 2 (ct & 3), +1 of rows r0 and r0 + 4 of strip ct / 4 -- of the
+  // first block's slot in lanes 0-31 (k 0-15), the second's in lanes 32-63 (k 16-31)
+  int off1[2], off2[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) off1[s2] = i * 128 + ((4 * s2 + g) ^ sw(i)) * 16;
+  {
+    const int r0 = 8 * (g & 1) + qq;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) off2[c4] = r0 * 128 + ((2 * c4 + (p4 >> 1)) ^ sw(r0)) * 16 + 8 * (p4 & 1);
+  }
+  const uint8_t* p2base = g < 2 ? my0 : my1;
+
+  // -I as the B operand of iterate tile t: lane (i, g) holds k = 8g .. 8g + 7 of column n = i
+  bf16x8 NEGI[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) NEGI[t][j] = (8 * g + j == 16 * t + i) ? (__bf16)(-1.0f) : (__bf16)(0.0f);
+
+  constexpr int AD = MPA_LSQP4_AD;
+  // phase 1 of one block: P_w[rows 4g + r][iterate 16 t + i], starting from -B (wave 0) or 0
+  auto phase1 = [&](int b, uint8_t* slot, uint8_t* bslot, f32x4 (&p1)[2]) __attribute__((always_inline)) {
+    wait_strip(b, (AD - 1) / 2);
+    {
+      const bf16x8 bfr = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+          (w == 0 ? bslot : &bzero[w][0]) + i * (PH * 2) + 16 * g));
+      p1[0] = mfma_v0(bfr, NEGI[0]);
+      p1[1] = mfma_v0(bfr, NEGI[1]);
+    }
+    bf16x8 af[AD];
+    auto rd1 = [&](int s) __attribute__((always_inline)) {
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + off1[s & 1] + 2048 * (s >> 1)));
+    };
+#pragma unroll
+    for (int s = 0; s < AD; ++s) af[s] = rd1(s);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + AD < NKS && ((s + AD) & 1) == 0) wait_strip(b, (s + AD) / 2);
+      mfma_v(p1[0], af[s % AD], XF[s][0]);
+      mfma_v(p1[1], af[s % AD], XF[s][1]);
+      if (s + AD < NKS) af[s % AD] = rd1(s + AD);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_v_settle(p1[0], p1[1]);
+  };
+
+  constexpr int CH = 4;
+  auto pstep = [&](int u) __attribute__((always_inline)) {
+    f32x4 p1a[2], p1b[2];
+    phase1(0, my0, bring[0], p1a);
+    phase1(1, my1, bring[1], p1b);
+    // phase 2's first chunk of transposed reads before the barrier (they read this wave's slots)
+    s16x4 tb[2][CH][2];
+    auto rd = [&](int c, s16x4 (&d)[CH][2]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const uint8_t* src = p2base + off2[k] + 2048 * c;
+        d[k][0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(src));
+        d[k][1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(src + 4 * 128));
+      }
+    };
+    rd(0, tb[0]);
+    part[w][0][0][lane] = p1a[0];
+    part[w][0][1][lane] = p1a[1];
+    part[w][1][0][lane] = p1b[0];
+    part[w][1][1][lane] = p1b[1];
+    barrier();
+    // ---- reduce both blocks: R = sum of the four partials (wave order; wave 0's carry -B), bf16
+    // hi + lo; RF_hi[t] lane (i, g) = k 8g .. 8g + 7 = hi_u rows 0-7 | hi_u 8-15 | hi_u+1 0-7 |
+    // hi_u+1 8-15, RF_lo the same of the lo halves: lsqp4's two lane swaps with (hi_u, hi_u+1) and
+    // (lo_u, lo_u+1) in place of (hi, lo).  A pair past the range's end (odd block count) zeroes the
+    // second block's residual: its slot holds the range's last block again, which then adds 0.
+    const bool second = u + 1 < nb;  // wave-uniform
+    bf16x8 RFH[2], RFL[2];
+    {
+      f32x4 pv[2][2][QW];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int ww = 0; ww < QW; ++ww) pv[b][t][ww] = part[ww][b][t][lane];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        uint32_t H[2][2], L[2][2];  // [block][d]
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          f32x4 v = pv[b][t][0];
+#pragma unroll
+          for (int ww = 1; ww < QW; ++ww) v += pv[b][t][ww];
+          if (b == 1 && !second) v = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            H[b][d] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2 * d], v[2 * d + 1]}, bf16x2));
+            const float h0 = __uint_as_float(H[b][d] << 16), h1 = __uint_as_float(H[b][d] & 0xffff0000u);
+            L[b][d] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2 * d] - h0, v[2 * d + 1] - h1}, bf16x2));
+          }
+        }
+        uint32_t XH[2], YH[2], XL[2], YL[2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto sa = __builtin_amdgcn_permlane32_swap(H[0][d], H[1][d], false, false);
+          const auto sb = __builtin_amdgcn_permlane16_swap(sa[0], sa[1], false, false);
+          XH[d] = sb[0];
+          YH[d] = sb[1];
+          const auto la = __builtin_amdgcn_permlane32_swap(L[0][d], L[1][d], false, false);
+          const auto lb = __builtin_amdgcn_permlane16_swap(la[0], la[1], false, false);
+          XL[d] = lb[0];
+          YL[d] = lb[1];
+        }
+        RFH[t] = __builtin_bit_cast(bf16x8, make_uint4(XH[0], XH[1], YH[0], YH[1]));
+        RFL[t] = __builtin_bit_cast(bf16x8, make_uint4(XL[0], XL[1], YL[0], YL[1]));
+      }
+    }
+    barrier();  // every wave's partial reads are done before any wave stores the next pair's
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase 2 of the pair: G_w^T[it][col] += sum_k R-image[it][k] A[row(k)][col], k over the
+    // pair's 32 rows, hi then lo; strip c of both slots is refilled with the next pair's once
+    // chunk c's MFMAs have consumed its reads
+    dma_b(kb0 + u + 2, bring[0]);
+    dma_b(kb0 + u + 3, bring[1]);
+    const Blk n0 = blk(kb0 + u + 2), n1 = blk(kb0 + u + 3);
+#pragma unroll
+    for (int c = 0; c < NCT / CH; ++c) {
+      lgkm_wait<0>();  // this chunk's reads, issued during the previous chunk's MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 1 < NCT / CH) rd(c + 1, tb[(c + 1) & 1]);
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const bf16x8 bt = __builtin_bit_cast(
+            bf16x8, __builtin_shufflevector(tb[c & 1][k][0], tb[c & 1][k][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        G[0][CH * c + k] = mfma(RFH[0], bt, G[0][CH * c + k]);
+        G[1][CH * c + k] = mfma(RFH[1], bt, G[1][CH * c + k]);
+        G[0][CH * c + k] = mfma(RFL[0], bt, G[0][CH * c + k]);
+        G[1][CH * c + k] = mfma(RFL[1], bt, G[1][CH * c + k]);
+      }
+      if (c + 1 < NCT / CH) {
+#pragma unroll
+        for (int j = 0; j < 2 * CH; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // two MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      dma_strip(n0, vfull, vpart, c, my0);
+      dma_strip(n1, vfull, vpart, c, my1);
+    }
+    pf(kb0 + u + 2 + pfd);
+    pf(kb0 + u + 3 + pfd);
+  };
+  for (int u = 0; u < nb; u += 2) pstep(u);
+#undef MPA_VMCNT
+  drain_vm();  // the trailing (unused) DMA pieces
+
+  // ---- G over the row groups: fan-in-PF tree per (half, wave) of write-through partials
+  const int nct = 2 * nks;
+  const size_t wslab = size_t(2 * NCT) * 64;  // f32x4 units of one wave's partial
+  f32x4* __restrict__ slab = static_cast<f32x4*>(a.slab) + (size_t(h) * kLsqpMaxGroups * QW + w) * wslab;
+  const size_t qstride = size_t(QW) * wslab;  // between consecutive row groups
+  uint32_t* ctr = a.ctr + (h * QW + w) * kLsqpCtrPerSlice;
+  float* out = static_cast<float*>(a.out);
+  auto store_out = [&](int t, int ct, const f32x4& v) __attribute__((always_inline)) {
+    const int col = c0 + 16 * ct + i;
+    if (ct < nct && col < cols)
+      *reinterpret_cast<f32x4*>(out + size_t(col) * K + PH * h + 16 * t + 4 * g) = v;
+  };
+  bool cx = false;
+  if (ng == 1) {
+    cx = disarmed(a.go, a.seq);
+    if (!cx)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) store_out(t, ct, G[t][ct]);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) st_wt(slab + size_t(q) * qstride + (t * NCT + ct) * 64 + lane, G[t][ct]);
+    unsigned idx = unsigned(q), count = unsigned(ng), stride = 1;
+    int lvl_off = 0, lvl_cap = (kLsqpMaxGroups + PF - 1) / PF;
+    for (;;) {
+      drain_vm();
+      const unsigned first = (idx / PF) * PF;
+      const unsigned gsize = count - first < unsigned(PF) ? count - first : unsigned(PF);
+      unsigned old = 0;
+      if (lane == 0) {
+        uint32_t* c = &ctr[lvl_off + int(idx / PF)];
+        old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == gsize) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      old = __shfl(old, 0, 64);
+      if (old + 1 != gsize) return;  // an earlier arriver of the group: the last one carries it
+      const unsigned next = (count + PF - 1) / PF;
+      if (next == 1) cx = disarmed(a.go, a.seq);
+      const f32x4* src = slab + size_t(first) * stride * qstride;
+#pragma unroll 4
+      for (int j2 = 0; j2 < 2 * NCT; ++j2) {
+        const int j = j2 * 64 + lane;
+        f32x4 s = ld_wt(src + j);
+        for (unsigned m = 1; m < gsize; ++m) s += ld_wt(src + size_t(m) * stride * qstride + j);
+        if (next == 1) {
+          if (!cx) store_out(j2 / NCT, j2 % NCT, s);
+        } else {
+          st_wt(slab + size_t(first) * stride * qstride + j, s);
+        }
+      }
+      if (next == 1) break;
+      idx /= PF;
+      count = next;
+      stride *= PF;
+      lvl_off += lvl_cap;
+      lvl_cap = (lvl_cap + PF - 1) / PF;
+    }
+  }
+  // this slice of G is written: the task's last slice (2 halves x 4 waves) publishes
+  drain_vm();
+  if (lane == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    drain_vm();
+    const unsigned old = __hip_atomic_fetch_add(&a.ctr[2 * 8 * kLsqpCtrPerSlice], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == unsigned(2 * QW)) {
+      __hip_atomic_store(&a.ctr[2 * 8 * kLsqpCtrPerSlice], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!cx) publish_done(a.flag, a.seq);  // every slice read the same go word
+    }
+  }
+}
+
+}  // namespace
+
+
+hipError_t launch_lsqp7(const LsqpBatch& a, hipStream_t s) {
+  const int pairs = a.grp0[a.ntasks];
+  if (pairs <= 0) return hipErrorInvalidValue;
+  bool full = true;
+  for (int t = 0; t < a.ntasks; ++t) full = full && a.t[t].cols == kLsqpMaxCols && a.t[t].rows % PRB == 0;
+  if (!full) return launch_lsqp4(a, s);  // the pair step is written for the FULL form only
+  const int grid = (pairs + 7) / 8 * 16;
+  if (batch_armed(a)) hipLaunchKernelGGL((lsqp7_kernel<true>), dim3(grid), dim3(QT), 0, s, a);
+  else hipLaunchKernelGGL((lsqp7_kernel<false>), dim3(grid), dim3(QT), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace mpa
