@@ -70,10 +70,11 @@ void Comm::gate(int kind) {
   const uint64_t t0_ns = uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count());
   for (int64_t j = a; j < e; ++j) {
     const int64_t r = gate_ranks_[size_t(j)];
+    PoliteSpin poll;  // hot, then sleeping between polls (comm.hpp)
     for (uint64_t spins = 0; gate_finished(r) < gate_rel_[size_t(r - 1)]; ++spins) {
       if ((spins & 0xFFF) == 0xFFF)
         gate_poll(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
-      std::this_thread::yield();
+      poll();
     }
     gate_seen(r, gate_rel_[size_t(r - 1)], t0_ns);
   }

@@ -49,26 +49,6 @@ extern const bool g_wait_value_ops;
 
 using Clock = std::chrono::steady_clock;
 
-// A polite poll for the transport's long waits: pause for the first kHotSpinNs of a wait (c1's
-// epochs wait microseconds: no system call on that path), then yield the core on every poll.  The
-// coordinator's wait and the straggler timer's final spin are two busy threads of one process; on
-// a core they share, a bare pause loop keeps the other one off until the scheduler's time slice
-// ends, and the gated replays saw harvests up to 1.1 ms -- the timer's spin -- behind their
-// trigger (profiles/r05_gated_hops.txt).  With yields they alternate within microseconds.
-constexpr int64_t kHotSpinNs = 50000;
-struct PoliteSpin {
-  Clock::time_point t0 = Clock::now();
-  uint32_t n = 0;
-  bool cold = false;
-  void operator()() {
-    if (cold) {
-      std::this_thread::yield();
-      return;
-    }
-    __builtin_ia32_pause();
-    if ((++n & 63) == 0 && Clock::now() - t0 > std::chrono::nanoseconds(kHotSpinNs)) cold = true;
-  }
-};
 // workgroups per least-squares launch: 192 (24 per XCD, 3/4 of the CUs) streams the c2
 // batch at 7.1-7.2 TB/s against 6.7-6.8 at 512 and 7.0 at 256 (profiles/r01_tune_sweep4_grid.jsonl,
 // same-box bench A/B in profiles/r01_lsq_grid_ab.txt: c2 +6-7 %, c3/c4 unchanged); the read
