@@ -20,23 +20,19 @@
 namespace mpa {
 
 // A polite poll for the transport's long waits: pause for the first kHotSpinNs of a wait (c1's
-// epochs wait microseconds: no system call on that path), then sleep kColdPollNs between polls.
-// The coordinator's wait and the straggler timer's final spin are two busy threads of one
-// process; on a core they share, a bare pause loop keeps the other one off until the scheduler's
-// time slice ends, and the gated replays saw harvests up to 1.1 ms -- the timer's spin -- behind
-// their trigger (profiles/r05_gated_hops.txt).  Yielding instead still left 0.98 ms (a yield is no
-// promise to run the other thread first); a thread that sleeps between polls is the one the
-// scheduler runs at once when it wakes.  The cost is up to a poll interval plus the wake-up on
-// waits that already last over 50 us (c2's host waits overlap the next launched epoch).
+// epochs wait microseconds: no system call on that path), then yield the core on every poll.  The
+// coordinator's wait and the straggler timer's final spin are two busy threads of one process; on
+// a core they share, a bare pause loop keeps the other one off until the scheduler's time slice
+// ends.  (Sleeping between polls instead -- 20 us asked, ~60 us of timer slack got -- moved the
+// gated replays' median harvest from 4 to 42 us and their worst from 1.0 to 1.5 ms: r05o.)
 constexpr int64_t kHotSpinNs = 50000;
-constexpr int64_t kColdPollNs = 20000;
 struct PoliteSpin {
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   uint32_t n = 0;
   bool cold = false;
   void operator()() {
     if (cold) {
-      std::this_thread::sleep_for(std::chrono::nanoseconds(kColdPollNs));
+      std::this_thread::yield();
       return;
     }
     __builtin_ia32_pause();

@@ -930,7 +930,8 @@ void HipComm::calibrate(int64_t* ticks, int64_t* ns) {
 
 void HipComm::set_trace(int64_t capacity) {
   if (capacity < 0) fail(MPA_ARGUMENT_ERROR, "trace capacity < 0");
-  HIPCHECK(hipDeviceSynchronize());  // no task still stamps the old buffer
+  drain_deferred();                  // no timer-deferred launch still holds an entry of the old buffer
+  HIPCHECK(hipDeviceSynchronize());  // no task still stamps it
   for (auto& w : w_) w.tslot = -1;
   if (trace_) HIPCHECK(hipHostFree(trace_));
   trace_ = nullptr;
