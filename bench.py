@@ -342,8 +342,9 @@ def report(args, cfg, world, el, per_rank, extra):
     return out
 
 
-ROCPROF_STATS = {"c2": ("r04_c2_kernel_stats.csv", "lsq_grad_kernel"),
-                 "c5": ("r04_c5_kernel_stats.csv", "lsqp4_kernel")}
+ROCPROF_STATS = {"c2": ("%s_c2_kernel_stats.csv", "lsq_grad_kernel"),
+                 "c5": ("%s_c5_kernel_stats.csv", "lsqp4_kernel")}
+PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")   # newest first
 
 
 def rocprof_avg_ms(cfg):
@@ -351,10 +352,15 @@ def rocprof_avg_ms(cfg):
     profiles of this config's bench command: the timed-region window of its kernel trace
     (tools/trace_window.py) of the newest round that has one, else the --stats summary; None
     without either."""
-    name, kernel = ROCPROF_STATS.get(cfg["config"], (None, None))
-    for rnd in ("r04", "r03", "r02"):
+    pattern, kernel = ROCPROF_STATS.get(cfg["config"], (None, None))
+    name = None
+    for rnd in PROFILE_ROUNDS:
+        if pattern and os.path.exists(os.path.join(ROOT, "profiles", pattern % rnd)):
+            name = pattern % rnd
+            break
+    for rnd in PROFILE_ROUNDS:
         win = os.path.join(ROOT, "profiles", "%s_%s_rocprof_window.json" % (rnd, cfg["config"]))
-        if name and os.path.exists(win):
+        if pattern and os.path.exists(win):
             d = json.load(open(win))
             if d.get("kernel") == kernel:
                 return round(d["avg_ms"], 4), "profiles/%s (last %d launches of the traced run = its timed region; %s)" % (
