@@ -158,7 +158,11 @@ int mpa_waitall(mpa_pool* pool,
 int mpa_comm_create(int transport, int64_t nworkers, const int* devices, mpa_comm** out);
 void mpa_comm_destroy(mpa_comm* comm);
 int64_t mpa_comm_size(const mpa_comm* comm); /* nworkers + 1, as MPI.Comm_size */
-/* coordinator stream (hipStream_t); NULL = the device's null stream */
+/* coordinator stream (hipStream_t).  NULL (the legacy default stream) selects the comm's own
+ * coordinator stream: a blocking stream, so HIP orders it with the caller's NULL-stream work
+ * both ways, while the comm's epoch steps and harvests no longer wait, as every NULL-stream
+ * command does, for the stragglers' tasks running on the worker streams (MPA_OWN_COORD=0:
+ * the NULL stream itself). */
 int mpa_comm_set_stream(mpa_comm* comm, void* stream);
 /* worker tasks (rank in 1..nworkers) */
 int mpa_comm_set_task_kmap(mpa_comm* comm, int64_t rank, int task /* ECHO/KMAP1/KMAP2 */);

@@ -24,12 +24,12 @@ int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares la
 // stream_shared()).
 // Past the cap a stream is only shared with streams of its own kind: a launch stream never
 // carries a worker's (possibly sleeping, delayed) tasks, so a batch never queues behind an
-// unrelated straggler.
+// unrelated straggler, and a coordinator stream never carries tasks.
 struct QueueStream {
   int device;
   hipStream_t s;
   int users;
-  bool launch;
+  StreamKind kind;
 };
 std::mutex g_stream_mu;
 std::vector<QueueStream> g_streams;
@@ -53,7 +53,7 @@ void destroy_pooled_streams() {
   g_streams.clear();
 }
 
-hipStream_t make_queue_stream(int device, bool launch) {
+hipStream_t make_queue_stream(int device, StreamKind kind) {
   static const bool registered = (std::atexit(destroy_pooled_streams), true);
   (void)registered;
   std::lock_guard<std::mutex> lk(g_stream_mu);
@@ -62,7 +62,7 @@ hipStream_t make_queue_stream(int device, bool launch) {
     if (q.device == device) {
       if (q.users == 0) {
         q.users = 1;
-        q.launch = launch;
+        q.kind = kind;
         return q.s;
       }
       ++have;
@@ -70,7 +70,7 @@ hipStream_t make_queue_stream(int device, bool launch) {
   if (have >= queue_cap()) {  // share the least-used one of the same kind
     QueueStream* best = nullptr;
     for (auto& q : g_streams)
-      if (q.device == device && q.launch == launch && (!best || q.users < best->users)) best = &q;
+      if (q.device == device && q.kind == kind && (!best || q.users < best->users)) best = &q;
     if (best) {
       best->users += 1;
       return best->s;
@@ -83,7 +83,7 @@ hipStream_t make_queue_stream(int device, bool launch) {
   if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
   hipStream_t s = nullptr;
   HIPCHECK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
-  g_streams.push_back({device, s, 1, launch});
+  g_streams.push_back({device, s, 1, kind});
   return s;
 }
 

@@ -87,7 +87,8 @@ inline int lsqb_grid(int pass) {
 // ~10 ms), so a destroyed comm returns its streams and the next comm reuses them; past the
 // cap (MPA_MAX_QUEUES) streams are shared.
 constexpr int kDefaultMaxQueues = 12;
-hipStream_t make_queue_stream(int device, bool launch);
+enum class StreamKind { kWorker, kLaunch, kCoord };
+hipStream_t make_queue_stream(int device, StreamKind kind);
 void release_queue_stream(int device, hipStream_t s);
 bool stream_shared(hipStream_t s);  // more than one worker / comm launches on it
 int queue_streams(int device);      // CU-masked streams the process holds on the device
@@ -215,7 +216,14 @@ class HipComm final : public Comm {
   ~HipComm() override;
 
   int transport() const override { return MPA_TRANSPORT_HIP; }
-  void set_stream(hipStream_t s) { coord_ = s; }
+  // The coordinator stream.  The legacy default stream (NULL, torch's default) is replaced by
+  // the comm's own stream: HIP orders every command of the NULL stream after all the work
+  // queued on the device's blocking streams, the worker streams included, so an epoch step
+  // or a stale harvest on it waited for the stragglers' running tasks (c3: 0.1-0.6 ms per
+  // epoch step, up to 5.7 ms per harvest; profiles/r05_null_stream.txt).  The comm's stream is
+  // a blocking stream itself, so HIP still orders it with the caller's NULL-stream work both
+  // ways.  MPA_OWN_COORD=0 keeps the NULL stream.
+  void set_stream(hipStream_t s) { coord_ = (s == nullptr || s == hipStreamLegacy) && own_coord_ ? own_coord_ : s; }
   hipStream_t stream() const { return coord_; }
 
   void begin_call(const CallBufs& b) override {
@@ -524,12 +532,12 @@ class HipComm final : public Comm {
 
   // the worker's own stream (delayed tasks, pre-armed tasks), created on first use
   hipStream_t worker_stream(HipWorker& w) {
-    if (!w.stream) w.stream = make_queue_stream(dev_, /*launch=*/false);
+    if (!w.stream) w.stream = make_queue_stream(dev_, StreamKind::kWorker);
     return w.stream;
   }
   // launch stream k (created on first use, up to kLaunchStreams)
   hipStream_t launch_stream(size_t k) {
-    while (launch_streams_.size() <= k) launch_streams_.push_back(make_queue_stream(dev_, /*launch=*/true));
+    while (launch_streams_.size() <= k) launch_streams_.push_back(make_queue_stream(dev_, StreamKind::kLaunch));
     return launch_streams_[k];
   }
 
@@ -694,6 +702,7 @@ class HipComm final : public Comm {
   int my_rank_ = 0;
   int dev_ = 0;
   hipStream_t coord_ = nullptr;
+  hipStream_t own_coord_ = nullptr;  // the coordinator stream in place of the NULL stream (set_stream)
   unsigned long long* flags_ = nullptr;
   unsigned* err_ = nullptr;
   unsigned* err_dev_ = nullptr;

@@ -107,6 +107,8 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   } else if (role_ == SERVER && here_count > 1) {
     launch_stream(kLaunchStreams - 1);
   }
+  // the coordinator's own stream, in place of the NULL stream (set_stream)
+  if (role_ != SERVER && !env_off("MPA_OWN_COORD")) coord_ = own_coord_ = make_queue_stream(dev_, StreamKind::kCoord);
   HIPCHECK(hipEventCreateWithFlags(&xfer_ev_, hipEventDisableTiming));
   int khz = 0;
   HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
@@ -192,6 +194,7 @@ HipComm::~HipComm() {
     if (w.stream) release_queue_stream(dev_, w.stream);
   }
   for (auto& s : launch_streams_) release_queue_stream(dev_, s);
+  if (own_coord_) release_queue_stream(dev_, own_coord_);
   for (auto& t : timed_) {
     (void)hipEventDestroy(t.start);
     (void)hipEventDestroy(t.stop);
