@@ -56,6 +56,12 @@ CONFIGS = {
                desc="BASELINE configs[3] shape: fp64 A 2^23x2048 (16 GiB per worker), nwait = "
                     "worker 1 fresh + 5 others (test/kmap2.jl:65 style predicate), stale results folded in "
                     "at weight 0.5, Exp(1 ms) delays"),
+    # measurement shapes, not bench lines: c3's / c4's tasks with nwait = n and no delays, one
+    # batched launch per epoch, so the kernel line is the shard kernel's own roofline
+    "c3k": dict(rows=1 << 23, cols=2048, workers=8, nwait=8, dtype="f32", timing_period=1,
+                desc="measurement: c3's fp32 2^23x2048 tasks, nwait=8, no delays (kernel roofline)"),
+    "c4k": dict(rows=1 << 23, cols=2048, workers=8, nwait=8, dtype="f64", timing_period=1,
+                desc="measurement: c4's fp64 2^23x2048 tasks, nwait=8, no delays (kernel roofline)"),
     "c5": dict(rows=1 << 23, cols=2048, workers=8, nwait=7, dtype="bf16", iterates=64,
                desc="BASELINE configs[4] shape: batched 64-iterate variant, bf16 A 2^23x2048 "
                     "(4 GiB per worker), X 2048x64, fp32 accumulate (MFMA), nwait=7"),

@@ -209,6 +209,47 @@ def test_device_delays_only_on_unshared_streams(M, torch_mod, monkeypatch):
     c.close()
 
 
+def _straggler_hold(M, torch):
+    """Three nwait = 1 calls while worker 2's 400 ms delay sleeps ON THE DEVICE (a sleep kernel on
+    its worker stream): the wall time of each call."""
+    import time
+    c = M.DeviceComm(2)
+    for r in (1, 2):
+        c.set_task(r, "kmap2")
+    c.set_delays(2, [400_000_000])
+    pool = M.MPIAsyncPool(2)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    s, rb, isb = torch.ones(1, **f64), torch.zeros(6, **f64), torch.zeros(2, **f64)
+    irb = torch.zeros_like(rb)
+    t = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        M.asyncmap_(pool, s, rb, isb, irb, c, nwait=1)
+        t.append(time.perf_counter() - t0)
+    sleeps = c.counter("sleeps")
+    M.waitall_(pool, rb, irb)
+    ok = rb.cpu().numpy().reshape(2, 3)[:, 0].tolist() == [1.0, 2.0]
+    c.close()
+    return t, sleeps, ok
+
+
+def test_running_straggler_does_not_hold_the_coordinator(M, torch_mod, monkeypatch):
+    """k-of-n: a straggler's task RUNNING on its worker stream must not hold the coordinator's
+    work.  The Python API hands the comm torch's default stream, HIP's NULL stream, and HIP runs
+    a NULL-stream command only after everything queued on the device's blocking streams: the
+    exchange that re-dispatched worker 1 waited for worker 2's running kernel (c3: 0.1-0.6 ms per
+    epoch step, up to 5.7 ms per harvest; profiles/r05_null_stream.txt).  The comm coordinates on
+    a stream of its own instead (hip_transport.hpp set_stream): calls 2 and 3 re-dispatch worker 1
+    in milliseconds while worker 2's 400 ms sleep kernel runs."""
+    monkeypatch.setenv("MPA_DELAY", "device")
+    torch = torch_mod
+    t, sleeps, ok = _straggler_hold(M, torch)
+    assert sleeps == 1 and ok
+    assert max(t[1:]) < 0.1, t
+    monkeypatch.setenv("MPA_OWN_COORD", "0")  # the NULL stream, for the record
+    print("re-dispatch call times (s): own stream %s; NULL stream %s" % (t, _straggler_hold(M, torch)[0]))
+
+
 @pytest.mark.timing
 def test_delay_calibration(M, torch_mod):
     """An injected delay of d ms shows up as a latency of d ms (within 0.5 ms)."""
