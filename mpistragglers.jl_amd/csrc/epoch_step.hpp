@@ -101,6 +101,57 @@ __device__ __forceinline__ H16<V> ld_bf16(const uint16_t* p) {
   }
 }
 
+// System-scope write-through stores (sc0 sc1: the bytes go to memory instead of sitting dirty in
+// this XCD's L2) of the messages other processes read.  Once every storing wave has drained
+// them (s_waitcnt vmcnt(0)) they are visible at system scope, so the doorbell behind them needs
+// no L2 writeback: a system-scope release fence in every workgroup wrote back each XCD's whole
+// L2 (the recvbuf, x and mirror stores of the step too) before the doorbells could ring.
+typedef unsigned SysU4 __attribute__((ext_vector_type(4)));
+typedef unsigned SysU2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_sys(void* p, uint4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(__builtin_bit_cast(SysU4, v)) : "memory");
+}
+__device__ __forceinline__ void st_sys(void* p, uint2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(__builtin_bit_cast(SysU2, v)) : "memory");
+}
+__device__ __forceinline__ void st_sys(void* p, unsigned v) {
+  asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sys(void* p, unsigned short v) {
+  asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"(p), "v"(unsigned(v)) : "memory");
+}
+template <typename T, int V>
+__device__ __forceinline__ void est_sys(T* p, const EVec<T, V>& v) {
+  if constexpr (V * sizeof(T) == 16) {
+    st_sys(p, __builtin_bit_cast(uint4, v));
+  } else if constexpr (V * sizeof(T) == 8) {
+    st_sys(p, __builtin_bit_cast(uint2, v));
+  } else if constexpr (V * sizeof(T) == 32) {
+    struct U2 {
+      uint4 a, b;
+    };
+    const U2 u = __builtin_bit_cast(U2, v);
+    st_sys(p, u.a);
+    st_sys(reinterpret_cast<uint4*>(p) + 1, u.b);
+  } else {
+    static_assert(V * sizeof(T) == 4, "4-, 8-, 16- or 32-B vectors");
+    st_sys(p, __builtin_bit_cast(unsigned, v));
+  }
+}
+template <int V>
+__device__ __forceinline__ void st_bf16_sys(uint16_t* p, const H16<V> h) {
+  if constexpr (V == 8) {
+    st_sys(p, __builtin_bit_cast(uint4, h));
+  } else if constexpr (V == 4) {
+    st_sys(p, __builtin_bit_cast(uint2, h));
+  } else if constexpr (V == 2) {
+    st_sys(p, __builtin_bit_cast(unsigned, h));
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e) st_sys(p + e, h.v[e]);
+  }
+}
+
 // relaxed agent-scope element store / load: write-through to the coherence point, visible to
 // workgroups on other XCDs without an L2 writeback / invalidate (the fused head's messages)
 template <typename T>
@@ -170,7 +221,10 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
       } else {
         h = ld_bf16<V>(a.mirror + j);
       }
-      for (int d = 0; d < a.ndst; ++d) st_bf16<V>(reinterpret_cast<uint16_t*>(a.dst[d]) + j, h);
+      for (int d = 0; d < a.ndst; ++d) {
+        if ((a.dst_sys >> d) & 1u) st_bf16_sys<V>(reinterpret_cast<uint16_t*>(a.dst[d]) + j, h);
+        else st_bf16<V>(reinterpret_cast<uint16_t*>(a.dst[d]) + j, h);
+      }
     } else {
       if (BF16 && a.update && a.mirror) {
         H16<V> h;
@@ -183,7 +237,8 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
 #pragma unroll
           for (int e = 0; e < V; ++e) st_agent(reinterpret_cast<T*>(a.dst[d]) + j + e, v.v[e]);
         } else {
-          est<T, V>(reinterpret_cast<T*>(a.dst[d]) + j, v);
+          if ((a.dst_sys >> d) & 1u) est_sys<T, V>(reinterpret_cast<T*>(a.dst[d]) + j, v);
+          else est<T, V>(reinterpret_cast<T*>(a.dst[d]) + j, v);
         }
       }
     }

@@ -143,20 +143,29 @@ template <typename T, int V>
 __global__ void __launch_bounds__(kThreads) epoch_kernel(EpochArgs a) {
   epoch_elems<T, V>(a, int64_t(blockIdx.x) * blockDim.x + threadIdx.x, int64_t(gridDim.x) * blockDim.x);
   if (a.ndoor == 0) return;
-  // as exchange_kernel: every block's stores drained and released at system scope, then the
-  // last block to arrive rings the doorbells
+  // every block's message stores drained, then the last block to arrive rings the doorbells.
+  // The remote messages went out write-through at system scope (EpochArgs::dst_sys): drained,
+  // they are visible to the other processes, and no block writes back its L2.  sys_fence
+  // (MPA_MSG_WT=0): plain stores, released at system scope by every block, as exchange_kernel.
   __shared__ unsigned s_last;
   drain_vm();
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence_system();
-    drain_vm();
+    if (a.sys_fence) {
+      __threadfence_system();
+      drain_vm();
+    }
     const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (old - a.ticket_base) == gridDim.x - 1;
     if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      for (int d = 0; d < a.ndoor; ++d)
-        __hip_atomic_store(a.door[d], a.doorval[d], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (a.sys_fence) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        for (int d = 0; d < a.ndoor; ++d)
+          __hip_atomic_store(a.door[d], a.doorval[d], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        for (int d = 0; d < a.ndoor; ++d)
+          __hip_atomic_store(a.door[d], a.doorval[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
 }

@@ -88,6 +88,12 @@ struct EpochArgs {
   unsigned long long doorval[kMaxDoorbells];
   uint32_t* ticket;
   uint32_t ticket_base;
+  // messages other processes read (remote workers' slots): bit k set = dst[k] is stored
+  // write-through at system scope (sc0 sc1), so the doorbells need no L2 writeback; sys_fence
+  // = 1 (MPA_MSG_WT=0): plain stores and a system-scope release in every workgroup instead
+  uint32_t dst_sys;
+  uint32_t sys_fence;
+  uint32_t reserved_[3];
 };
 // One worker task of a least-squares launch.
 struct LsqTask {

@@ -496,15 +496,21 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   if (batch.tail == 2) epoch_elems<T, E, false, false>(batch.ep, tid, kThreads);
   else epoch_elems<T, 1, false, false>(batch.ep, tid, kThreads);
   if (batch.ep.ndoor == 0) return;
-  // the next messages of remote workers are in their slots: release them at system scope,
-  // then ring the doorbells (as epoch_kernel's last block)
+  // the next messages of remote workers are in their slots (written through at system scope,
+  // EpochArgs::dst_sys; or plain and released here, sys_fence): ring the doorbells (as
+  // epoch_kernel's last block)
   drain_vm();
   __syncthreads();
   if (tid == 0) {
-    __threadfence_system();
-    drain_vm();
-    for (int d = 0; d < batch.ep.ndoor; ++d)
-      __hip_atomic_store(batch.ep.door[d], batch.ep.doorval[d], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (batch.ep.sys_fence) {
+      __threadfence_system();
+      drain_vm();
+      for (int d = 0; d < batch.ep.ndoor; ++d)
+        __hip_atomic_store(batch.ep.door[d], batch.ep.doorval[d], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      for (int d = 0; d < batch.ep.ndoor; ++d)
+        __hip_atomic_store(batch.ep.door[d], batch.ep.doorval[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 

@@ -138,6 +138,7 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   fused_head_ = !env_off("MPA_HEAD");
   prearm_ = fused_head_ && !env_off("MPA_PREARM");
   defer_ok_ = !env_off("MPA_DEFER");
+  msg_wt_ = !env_off("MPA_MSG_WT");
   pre_same_ = !env_off("MPA_PRESAME");
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&pre_mb_), sizeof(PreMailbox), hipHostMallocCoherent | hipHostMallocMapped));
   std::memset(static_cast<void*>(pre_mb_), 0, sizeof(PreMailbox));
@@ -681,11 +682,13 @@ EpochArgs HipComm::epoch_args(const std::vector<Harvest>& hv, size_t before, con
   a.x = u.x;
   a.mirror = u.mirror;
   a.msg_bf16 = u.msg_bf16 ? 1 : 0;
+  a.sys_fence = msg_wt_ ? 0u : 1u;
   for (const auto& d : stale_deferred_) a.dst0[a.ndst0++] = d.dst;  // (deferred_fit: callers check)
   for (int64_t rank : posted) {
     const HipWorker& w = w_[size_t(rank - 1)];
     a.dst[a.ndst++] = b_.isendbuf + size_t(w.slot) * b_.sl;
     if (w.remote) {
+      if (msg_wt_) a.dst_sys |= 1u << a.ndst;  // another process reads it: written through
       a.dst[a.ndst++] = msg_dst(w);
       a.door[a.ndoor] = w.box_door_dev;
       a.doorval[a.ndoor++] = w.seq;
