@@ -702,8 +702,8 @@ class HipComm final : public Comm {
   int my_rank_ = 0;
   int dev_ = 0;
   hipStream_t coord_ = nullptr;
-  hipStream_t own_coord_ = nullptr;
-  bool msg_wt_ = true;  // remote messages written through at system scope (EpochArgs::dst_sys)  // the coordinator stream in place of the NULL stream (set_stream)
+  hipStream_t own_coord_ = nullptr;  // the coordinator stream in place of the NULL stream (set_stream)
+  bool msg_wt_ = true;  // remote messages written through at system scope (EpochArgs::dst_sys)
   unsigned long long* flags_ = nullptr;
   unsigned* err_ = nullptr;
   unsigned* err_dev_ = nullptr;
