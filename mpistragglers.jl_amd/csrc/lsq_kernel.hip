@@ -620,6 +620,17 @@ int lsq_rows_per_wave_iter(int dtype, int cols) {
   return cp <= 256 ? 4 : cp <= 1024 ? 2 : 1;
 }
 
+#if MPA_MEASURE
+// the 2048-column shapes of c3 / c4 (measurement build, MPA_LSQ_V2048=<index>; 0 = shipped)
+static int v2048() {
+  static const int v = [] {
+    const char* e = std::getenv("MPA_LSQ_V2048");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+#endif
+
 const char* lsq_variant_name() { return kC2Variants[c2_variant()].name; }
 
 int lsq_set_variant(int i) {
@@ -636,7 +647,24 @@ hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s) {
       case 256: return go<float, 1, 4, kMode>(a, s);
       case 512: return go<float, 2, 4, kMode>(a, s);
       case 1024: return kC2Variants[c2_variant()].fn(a, s);
-      case 2048: return go<float, 8, 2, kMode>(a, s);
+      case 2048:
+#if MPA_MEASURE
+        switch (v2048()) {
+          case 1: return go<float, 8, 1, kMode>(a, s);
+          case 2: return go<float, 8, 4, kMode>(a, s);
+          case 3: return go<float, 8, 2, kMode | M_PREFETCH>(a, s);
+          case 4: return go<float, 8, 1, kMode | M_PREFETCH>(a, s);
+          case 5: return go<float, 8, 2, kMode | M_BLOCKED>(a, s);
+          default: break;
+        }
+#endif
+        // a batched launch of several tasks (one grid for all of them: nwait = n, no delays)
+        // streams 32 KiB per wave and tile: the c3 tasks batched (measurement config c3k) 0.76
+        // -> 0.83-0.90 of HBM; one task per launch (c3's delayed tasks, two to four launches
+        // overlapping) keeps 16 KiB and three waves per SIMD: -4 % with four rows
+        // (profiles/r05_lsq2048.txt)
+        if (a.ntasks >= 2) return go<float, 8, 4, kMode>(a, s);
+        return go<float, 8, 2, kMode>(a, s);
       default: return hipErrorInvalidValue;
     }
   }
@@ -651,7 +679,17 @@ hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s) {
       case 256: return go<double, 2, 4, kMode>(a, s);
       case 512: return go<double, 4, 2, kMode>(a, s);
       case 1024: return go<double, 8, 2, kMode>(a, s);
-      case 2048: return go<double, 16, 1, kMode>(a, s);
+      case 2048:
+#if MPA_MEASURE
+        switch (v2048()) {
+          case 1: return go<double, 16, 1, kMode | M_PREFETCH>(a, s);
+          case 2: return go<double, 16, 2, kMode>(a, s);
+          case 3: return go<double, 16, 1, kMode | M_BLOCKED>(a, s);
+          case 4: return go<double, 16, 1, M_CLAMP | M_DPP>(a, s);
+          default: break;
+        }
+#endif
+        return go<double, 16, 1, kMode>(a, s);
       default: return hipErrorInvalidValue;
     }
   }

@@ -312,6 +312,18 @@ def test_lsq_f32(M, torch_mod, rows, cols):
     assert err <= 1e-5, err
 
 
+@pytest.mark.parametrize("rows,cols", [(4099, 2048), (5000, 1536), (3, 2048)])
+def test_lsq_f32_batched_2048(M, torch_mod, rows, cols):
+    """Several fp32 tasks of up to 2048 columns in ONE launch take the four-row tile
+    (lsq_kernel.hip launch_lsq): every worker's gradient against the fp64 oracle at 1e-5, the
+    same bits for every worker (they share the shard)."""
+    out, g_ref, _ = _lsq_case(M, torch_mod, "f32", rows, cols, lda=((cols + 3) // 4) * 4, nworkers=3)
+    for w in range(3):
+        err = np.linalg.norm(out[w] - g_ref) / np.linalg.norm(g_ref)
+        assert err <= 1e-5, (w, err)
+    assert np.array_equal(out[0], out[1]) and np.array_equal(out[0], out[2])
+
+
 @pytest.mark.parametrize("rows,cols", [(1, 128), (300, 256), (1025, 1024), (999, 2048), (64, 130)])
 def test_lsq_f64(M, torch_mod, rows, cols):
     out, g_ref, _ = _lsq_case(M, torch_mod, "f64", rows, cols, lda=((cols + 1) // 2) * 2)
