@@ -556,6 +556,9 @@ constexpr Variant kC2Variants[] = {
     {go<float, 4, 2, M_CLAMP | M_DPP | M_PREFETCH | M_NT | M_BLOCKED>, 2, "rb2+clamp+dpp+prefetch+nt+blocked"},
     {go<float, 4, 4, M_CLAMP | M_DPP | M_PREFETCH | M_NT | M_BLOCKED>, 4, "rb4+clamp+dpp+prefetch+nt+blocked"},
     {go<float, 4, 8, M_CLAMP | M_DPP | M_NT | M_BLOCKED>, 8, "rb8+clamp+dpp+nt+blocked"},
+    // round 5: 32 KiB per wave and tile, as the batched 2048-column launch (profiles/r05_lsq2048.txt)
+    {go<float, 4, 8, M_CLAMP | M_DPP | M_NT>, 8, "rb8+clamp+dpp+nt"},
+    {go<float, 4, 6, M_CLAMP | M_DPP | M_NT>, 6, "rb6+clamp+dpp+nt"},
 #endif
 };
 constexpr int kNumC2Variants = int(sizeof(kC2Variants) / sizeof(kC2Variants[0]));
