@@ -454,8 +454,9 @@ def run_single(args, cfg):
     loop, x = make_loop(M, torch, cfg, pool, comm)
     _, recv, isend, irecv = loop.bufs
     extra = {}
-    if cfg["config"] == "c2":
-        # the same loop from Python (asyncmap_ + weights + lsq_update per step), reported beside
+    if cfg["config"] in ("c1", "c2"):
+        # the same loop from Python (asyncmap_ + weights + lsq_update per step), reported beside:
+        # what a caller driving asyncmap! itself per epoch (the reference's own loop) sees
         w = np.zeros(n)
 
         def step():

@@ -141,9 +141,17 @@ class DeviceComm(_Comm):
         torch.cuda.init()
         super().__init__(nworkers, devices)
 
+    _stream = None  # the stream last handed to the library
+
     def _before_call(self, sendbuf):
+        # torch's current stream (the raw handle: a Stream object costs microseconds per call),
+        # passed on only when it changed
         import torch
-        check(lib().mpa_comm_set_stream(self._h, C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        s = raw(torch.cuda.current_device()) if raw else torch.cuda.current_stream().cuda_stream
+        if s != self._stream:
+            check(lib().mpa_comm_set_stream(self._h, C.c_void_p(s)))
+            self._stream = s
 
     def set_task_lsq(self, rank, A, b, cols=None, lda=None):
         """g = A^T (A x - b) with A (rows x cols, row-major, leading dim lda) and b on the GPU."""

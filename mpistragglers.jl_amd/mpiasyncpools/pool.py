@@ -52,20 +52,34 @@ def check(rc):
         raise _EXC.get(rc, ErrorException)(_capi.last_error())
 
 
+_torch = None
+
+
+def _torch_mod():
+    global _torch
+    if _torch is None:
+        try:
+            import torch
+            _torch = torch
+        except ImportError:  # pragma: no cover
+            _torch = False
+    return _torch
+
+
 def buffer_info(a):
-    """(pointer, bytes, length, eltype name, isbits, is_device) of a numpy array or torch tensor."""
+    """(pointer, bytes, length, eltype, isbits, is_device) of a numpy array or torch tensor; the
+    eltype is the dtype object (str() names it).  Runs four times per asyncmap! call, so it
+    reads attributes only (the numpy ctypes view and str(dtype) cost a SIM call a third of its
+    time)."""
     if isinstance(a, np.ndarray):
         if not a.flags.c_contiguous:
             raise ArgumentError("buffers must be contiguous")
-        return a.ctypes.data, a.nbytes, a.size, str(a.dtype), a.dtype != object, False
-    try:
-        import torch
-    except ImportError:  # pragma: no cover
-        torch = None
-    if torch is not None and isinstance(a, torch.Tensor):
+        return a.__array_interface__["data"][0], a.nbytes, a.size, a.dtype, not a.dtype.hasobject, False
+    torch = _torch_mod()
+    if torch and isinstance(a, torch.Tensor):
         if not a.is_contiguous():
             raise ArgumentError("buffers must be contiguous")
-        return a.data_ptr(), a.numel() * a.element_size(), a.numel(), str(a.dtype), True, a.is_cuda
+        return a.data_ptr(), a.nbytes, a.numel(), a.dtype, True, a.is_cuda
     raise ArgumentError(f"unsupported buffer type {type(a).__name__}")
 
 
