@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "mpistragglers.jl_amd"))
 
 import numpy as np  # noqa: E402
 
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; the sparse headline is 2x)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 METRIC = "iterations/sec + shard-kernel HBM GB/s (% peak), nwait=k of 1/2/4/8 GPUs"
 
@@ -340,6 +341,19 @@ def report(args, cfg, world, el, per_rank, extra):
         out["roofline"]["committed_profiles"] = {
             "rocprof_avg_launch_ms": avg_ms, "source": src, "tree_commit": tree,
             "rocprof_frac": round(per_launch_bytes / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    if k > 1 and achieved:
+        # the batched variant's matrix-core side of the same launches: G = A^T (A X - B) is two
+        # bf16 products, 2 * 2 * rows * cols * k flops per task; lsqp4 issues 1.5x that (phase 2
+        # multiplies the hi and the lo bf16 halves of the fp32 residual, lsqp4_kernel.hip)
+        rt = rows // n
+        task_bytes = 2 * rt * cols + 2 * rt * k + 2 * cols * k + 4 * cols * k
+        flop_per_byte = 4.0 * rt * cols * k / task_bytes
+        alg_tf = achieved * 1e9 * flop_per_byte / 1e12
+        out["roofline"]["mfma"] = {
+            "alg_TFLOPs": round(alg_tf, 1), "issued_TFLOPs": round(1.5 * alg_tf, 1), "peak_TFLOPs": MFMA_BF16_PEAK_TFLOPS,
+            "frac_alg": round(alg_tf / MFMA_BF16_PEAK_TFLOPS, 4), "frac_issued": round(1.5 * alg_tf / MFMA_BF16_PEAK_TFLOPS, 4),
+            "note": "dense bf16 peak at 2.4 GHz (MI355X_MICROARCH.md); the 8-task launch holds 1.66 GHz in-kernel "
+                    "(power-limited, profiles/r05_c5_clock.txt), i.e. a clock-scaled peak of ~1730 TFLOP/s"}
     rp = extra.pop("measured_read_peak", None)
     if rp:
         out["roofline"]["measured_read_peak"] = rp
