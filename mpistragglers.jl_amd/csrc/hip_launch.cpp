@@ -18,7 +18,7 @@ int g_lsq_grid = 0;  // mpa_tune("lsq_grid", G): workgroups per least-squares la
 // process, p99 8.4 ms with 24, 34 of 150 launches > 1 ms with 32; the gated kmap2_n9 replay
 // ran within 1.5 ms of the oracle until a 24-worker comm grew the pool, then 578-643
 // harvests were 1-25 ms late (r04_gated_stall.txt).  So the process holds at most
-// queue_cap() of them per device (MPA_MAX_QUEUES, default 12, leaving room for the runtime's
+// queue_cap() of them per device (MPA_MAX_QUEUES, default 10, leaving room for the runtime's
 // and torch's own); a comm returns its streams here, the next one reuses them, and past the
 // cap workers share the least-used stream (a delayed worker then sleeps on a shared queue:
 // stream_shared()).

@@ -86,7 +86,7 @@ inline int lsqb_grid(int pass) {
 // resource (past ~20 per device the scheduler time-slices them and launches stall up to
 // ~10 ms), so a destroyed comm returns its streams and the next comm reuses them; past the
 // cap (MPA_MAX_QUEUES) streams are shared.
-constexpr int kDefaultMaxQueues = 12;
+constexpr int kDefaultMaxQueues = 10;  // 12 until round 5; the comm's own coordinator stream is one of them
 enum class StreamKind { kWorker, kLaunch, kCoord };
 hipStream_t make_queue_stream(int device, StreamKind kind);
 void release_queue_stream(int device, hipStream_t s);

@@ -161,21 +161,21 @@ def _warm_kernels(M, torch, n):
 
 
 def test_queue_cap(M, torch_mod):
-    """The process holds at most MPA_MAX_QUEUES (12) CU-masked streams per device: a comm of
+    """The process holds at most MPA_MAX_QUEUES (10) CU-masked streams per device: a comm of
     24 workers shares them, and a 9-worker comm after it gets a stream of its own per worker
-    (past ~20 queues the GPU time-slices them and launches stall ~10 ms,
-    profiles/r04_queue_latency.txt)."""
+    beside its coordinator stream (past ~20 queues the GPU time-slices them and launches stall
+    ~10 ms, profiles/r04_queue_latency.txt)."""
     big = M.DeviceComm(24)
     for r in range(1, 25):
         big.set_task(r, "kmap2")
-    assert big.counter("queues") <= 12
-    assert big.counter("shared_worker_streams") >= 12
+    assert big.counter("queues") <= 10
+    assert big.counter("shared_worker_streams") >= 14
     big.close()
     c = M.DeviceComm(9)
     for r in range(1, 10):
         c.set_task(r, "kmap2")
         c.set_delays(r, [1000])
-    assert c.counter("queues") <= 12 and c.counter("shared_worker_streams") == 0
+    assert c.counter("queues") <= 10 and c.counter("shared_worker_streams") == 0
     pool = M.MPIAsyncPool(9)
     torch = torch_mod
     rb = torch.zeros(27, dtype=torch.float64, device="cuda")
@@ -190,7 +190,7 @@ def test_device_delays_only_on_unshared_streams(M, torch_mod, monkeypatch):
     """MPA_DELAY=device (opt-in): a delayed task sleeps in a one-wave kernel ahead
     of it on its worker's stream -- but only where that stream is the worker's own: past the
     queue cap workers share streams, and a sleep there would hold the other worker's tasks,
-    so those delays stay on the host timer.  16 workers over 12 streams: one sleep kernel per
+    so those delays stay on the host timer.  16 workers over 9 streams: one sleep kernel per
     unshared worker, every reply correct."""
     monkeypatch.setenv("MPA_DELAY", "device")
     torch = torch_mod
@@ -203,7 +203,7 @@ def test_device_delays_only_on_unshared_streams(M, torch_mod, monkeypatch):
     M.asyncmap_(pool, torch.ones(1, dtype=torch.float64, device="cuda"), rb,
                 torch.zeros(16, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), c, nwait=16)
     shared = c.counter("shared_worker_streams")  # the streams were in place before the launches
-    assert 0 < shared < 16 and c.counter("queues") <= 12
+    assert 0 < shared < 16 and c.counter("queues") <= 10
     assert c.counter("sleeps") == 16 - shared, (c.counter("sleeps"), shared)
     assert rb.cpu().numpy().reshape(16, 3)[:, 0].tolist() == list(range(1, 17))
     c.close()
