@@ -165,3 +165,21 @@ def test_c1_mpi_cpu_baseline_runs():
     r = b.mpi_baseline(cfg, 1)
     assert r["kind"] == "mpi" and r["value"] > 100 and r["processes"] == 4 and r["cores"] == 4, r
     assert "3 worker processes over MPICH" in r["sample"]
+
+
+def test_c5_reports_its_matrix_core_side():
+    """The batched variant's line carries its MFMA figures beside the HBM roofline: two bf16
+    products (4 * rows * cols * k flops per task) at the HBM-measured rate, lsqp4 issuing 1.5x
+    that (phase 2 multiplies the hi and the lo halves of the residual), against the dense bf16
+    peak; the other configs carry none."""
+    cfg = _cfg("c5")
+    task = 4429971456.0  # one c5 task's algorithmic bytes (SURVEY.md §8d)
+    out = bench.report(_args(), cfg, 1, 1.0, [(100, 745.0, 100 * 8 * task, 745.0)], {})
+    r = out["roofline"]
+    m = r["mfma"]
+    flops_task = 4.0 * (1 << 20) * 2048 * 64
+    alg_tf = 8 * flops_task / 7.45e-3 / 1e12
+    assert abs(m["alg_TFLOPs"] - alg_tf) < 0.5 and abs(m["issued_TFLOPs"] - 1.5 * alg_tf) < 0.5
+    assert m["peak_TFLOPs"] == 2500.0 and abs(m["frac_issued"] - 1.5 * alg_tf / 2500.0) < 1e-3
+    assert abs(r["frac"] - 8 * task / 7.45e-3 / 1e9 / 8000.0) < 1e-3
+    assert "mfma" not in bench.report(_args(), _cfg("c2"), 1, 0.1, [(100, 60.0, 100 * 4299227136.0, 60.0)], {})["roofline"]
