@@ -34,6 +34,21 @@ __device__ __forceinline__ void publish_done(unsigned long long* flag, unsigned 
   __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Completion publish of a task whose reply stays in this GPU's memory and is read only by later
+// kernels on this GPU (the coordinator's own workers; the host reads nothing but the completion
+// word): the agent-scope release makes the reply visible on the device, and the word itself goes
+// out as a system-scope store, without publish_done's two system-scope L2 writebacks on every
+// task's completion path.  A reply another process or device reads keeps publish_done.
+__device__ __forceinline__ void publish_done_local(unsigned long long* flag, unsigned long long seq) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  drain_vm();
+  __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void publish_task(unsigned long long* flag, unsigned long long seq, int local) {
+  if (local) publish_done_local(flag, seq);
+  else publish_done(flag, seq);
+}
+
 // A pre-armed launch its server cancelled: the server's host-pinned cancel word holds the
 // task's seq (set before the doorbell wait is released, cleared once the stream has
 // drained, so every workgroup of the task reads the same value): return before any work.

@@ -300,6 +300,7 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
       a.out = w.out;
       a.rl = w.rl;
       a.pub = Publish{w.flag_dev, err_dev_, w.seq, spin_ticks()};
+      a.pub_local = pub_local();
       int64_t* e = trace_entry(w);
       a.stamp = e ? reinterpret_cast<unsigned long long*>(e + kTStart) : nullptr;
       go = [a, s, e]() {
@@ -491,6 +492,7 @@ LsqBatch HipComm::build_lsq_batch(const std::vector<int64_t>& ranks, int dtype, 
     t.lda = ts.lda;
     t.cols = int(ts.cols);
     t.grid = lsq_grid(ts, w, split);
+    t.pub_local = pub_local();
     if (ts.cols > kLsqWideSlice) {  // wide rows: pass-1 workgroups, pass-2 row groups
       const int nslice = int((ts.cols + kLsqWideSlice - 1) / kLsqWideSlice);
       const int es = dtype == MPA_F64 ? 8 : 4;
@@ -634,6 +636,7 @@ HipComm::LsqbLaunch HipComm::build_lsqb_batch(const std::vector<int64_t>& ranks,
       t.rows = ts.rows;
       t.lda = ts.lda;
       t.cols = int(ts.cols);
+      t.pub_local = pub_local();
       const int per = target / split + (k < target % split ? 1 : 0);
       const int64_t nblocks = (ts.rows + 15) / 16;
       const int ng = int(std::max<int64_t>(1, std::min<int64_t>(std::min(per, kLsqpMaxGroups), nblocks)));

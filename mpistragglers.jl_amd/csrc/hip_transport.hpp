@@ -704,6 +704,10 @@ class HipComm final : public Comm {
   hipStream_t coord_ = nullptr;
   hipStream_t own_coord_ = nullptr;  // the coordinator stream in place of the NULL stream (set_stream)
   bool msg_wt_ = true;  // remote messages written through at system scope (EpochArgs::dst_sys)
+  bool pub_local_ = true;  // MPA_PUB_LOCAL=0: every task publishes at system scope
+  // a task's reply stays on this GPU for this process's later kernels (SOLO, rank 0's own
+  // workers); a worker process's replies go to rank 0 (LsqTask::pub_local)
+  int pub_local() const { return pub_local_ && role_ != SERVER ? 1 : 0; }
   unsigned long long* flags_ = nullptr;
   unsigned* err_ = nullptr;
   unsigned* err_dev_ = nullptr;

@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(64) kmap_task_kernel(KmapArgs a) {
   drain_vm();
   __syncthreads();
   if (a.stamp && threadIdx.x == 0) __hip_atomic_store(a.stamp + 1, rt_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (threadIdx.x == 0) publish_done(a.pub.flag, a.pub.seq);
+  if (threadIdx.x == 0) publish_task(a.pub.flag, a.pub.seq, a.pub_local);
 }
 
 __global__ void __launch_bounds__(64) clock_probe_kernel(unsigned long long* out) {

@@ -120,6 +120,7 @@ struct LsqTask {
   void* r;
   uint32_t* wctr;
   int grid2;
+  int pub_local;  // the reply stays on this GPU: publish_done_local (device_common.hpp)
 };
 // Wide rows: two passes (r = A x - b, then g = A^T r over 2048-column slices), A read twice.
 constexpr int kLsqWideSlice = 2048;   // columns per slice (fp32: 8 x 16 B per lane, fp64: 16)
@@ -264,6 +265,7 @@ struct LsqpTask {
   // column pairs (lsqc_kernel.hip) only
   unsigned long long* xg;  // [kLsqpMaxGroups][2][kLsqcXR][4][64][4] {tag, fp32} exchange granules
   int parts;               // members per row group: 2 if cols > kLsqcMemberCols, else 1
+  int pub_local;  // as LsqTask::pub_local (lsqp4)
 };
 struct LsqpBatch {
   int ntasks;
@@ -373,6 +375,7 @@ struct KmapArgs {
   // task trace (host-pinned, may be null): [0] s_memrealtime at the kernel's start, [1] just
   // before its completion store
   unsigned long long* stamp;
+  int pub_local;  // as LsqTask::pub_local
 };
 // one wave stores s_memrealtime into *out (host-pinned): the task trace's clock calibration
 hipError_t launch_clock_probe(unsigned long long* out, hipStream_t s);

@@ -454,7 +454,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   drain_vm();
   __syncthreads();
   if (cx) return;
-  if (tid == 0) publish_done(a.flag, a.seq);
+  if (tid == 0) publish_task(a.flag, a.seq, a.pub_local);
   if (!batch.tail) return;
   // Fused tail: this workgroup finished its task (and published it); the last task of the
   // launch to finish runs the next epoch's coordinator step.  publish_done released the

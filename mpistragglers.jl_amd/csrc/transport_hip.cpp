@@ -139,6 +139,7 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   prearm_ = fused_head_ && !env_off("MPA_PREARM");
   defer_ok_ = !env_off("MPA_DEFER");
   msg_wt_ = !env_off("MPA_MSG_WT");
+  pub_local_ = !env_off("MPA_PUB_LOCAL");
   pre_same_ = !env_off("MPA_PRESAME");
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&pre_mb_), sizeof(PreMailbox), hipHostMallocCoherent | hipHostMallocMapped));
   std::memset(static_cast<void*>(pre_mb_), 0, sizeof(PreMailbox));
