@@ -8,6 +8,7 @@
 #include <string>
 
 #include "comm.hpp"
+#include "hip_transport.hpp"
 #include "kernels.hpp"
 #include "pool.hpp"
 
@@ -497,9 +498,12 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
       });
       if (rc != MPA_OK) return rc;
     }
-    rc = mpa_asyncmap(pool, msg, msg_bytes, recvbuf, recvbuf_bytes, recvbuf_bytes / reply_es, isendbuf, isendbuf_bytes,
-                      irecvbuf, irecvbuf_bytes, comm, nwait_kind, nwait, nwait_fn, nwait_ctx, "Int64", p.epoch + 1, 0,
-                      nullptr);
+    {
+      MPA_HPROF(mpa::kHpAsyncmap);
+      rc = mpa_asyncmap(pool, msg, msg_bytes, recvbuf, recvbuf_bytes, recvbuf_bytes / reply_es, isendbuf, isendbuf_bytes,
+                        irecvbuf, irecvbuf_bytes, comm, nwait_kind, nwait, nwait_fn, nwait_ctx, "Int64", p.epoch + 1, 0,
+                        nullptr);
+    }
     if (rc != MPA_OK) return rc;
     if (trace) {
       std::fprintf(stderr, "[mpa descent] epoch %lld repochs", (long long)p.epoch);
@@ -521,6 +525,7 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
     const double s = sum > 0 ? double(n) / sum : 0.0;
     for (auto& v : w) v *= s;
     if (fuse) {
+      MPA_HPROF(mpa::kHpUpdate);
       rc = guarded([&] {
         mpa::hip_stage_update(c, up.dtype, elems, w.data(), n, up.eta, up.x, up.mirror, up.msg_bf16);
       });
@@ -529,6 +534,19 @@ int descent_loop(mpa_pool* pool, mpa_comm* comm, const void* msg, size_t msg_byt
     }
     if (rc != MPA_OK) return rc;
   }
+#if MPA_MEASURE
+  if (const char* hp = std::getenv("MPA_HOST_PROF"); hp && *hp == '1') {
+    static const char* names[mpa::kHpKeys] = {"asyncmap", "flush", "pre_consume", "prearm", "launch call", "waitany",
+                                              "harvest", "post", "stage_update"};
+    std::fprintf(stderr, "[mpa host prof] %lld epochs, per epoch (us) / per call (us):\n", (long long)epochs);
+    for (int k = 0; k < mpa::kHpKeys; ++k) {
+      const int64_t ns = mpa::g_hprof.ns[k].exchange(0), cnt = mpa::g_hprof.n[k].exchange(0);
+      if (cnt)
+        std::fprintf(stderr, "  %-12s %8.2f / %8.2f  (%lld calls)\n", names[k], double(ns) / 1e3 / double(epochs > 0 ? epochs : 1),
+                     double(ns) / 1e3 / double(cnt), (long long)cnt);
+    }
+  }
+#endif
   if (fuse) {
     rc = guarded([&] {
       mpa::hip_set_ahead(c, 0, up.dtype, elems, w_all.data(), n, up.eta, up.x, up.mirror, up.msg_bf16);

@@ -44,6 +44,14 @@ __device__ __forceinline__ void publish_done_local(unsigned long long* flag, uns
   drain_vm();
   __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// As publish_done_local, for a reply every byte of which its writers stored write-through
+// (agent-scope relaxed stores: global_store sc1) and drained (s_waitcnt vmcnt(0)) before the
+// workgroup barrier that precedes this call: there is nothing left to release, and the
+// readers (the next step, after its own acquire) find the bytes past the L2s
+// (MI355X_MICROARCH.md, the "sc1 stores" valid form).
+__device__ __forceinline__ void publish_done_wt(unsigned long long* flag, unsigned long long seq) {
+  __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void publish_task(unsigned long long* flag, unsigned long long seq, int local) {
   if (local) publish_done_local(flag, seq);
   else publish_done(flag, seq);

@@ -839,7 +839,10 @@ void HipComm::enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s,
     }
     std::fflush(stderr);
   }
-  HIPCHECK(launch_lsq(dtype, cols, b, s));
+  {
+    MPA_HPROF(kHpLaunch);
+    HIPCHECK(launch_lsq(dtype, cols, b, s));
+  }
   if (debug_) {
     const hipError_t e = hipStreamSynchronize(s);
     std::fprintf(stderr, "[mpa role %d] lsq launch done: %s\n", int(role_), hipGetErrorString(e));

@@ -207,6 +207,30 @@ class ExchangeBuilder {
   hipStream_t s_;
 };
 
+// Host-side time per coordinator step (measurement build, MPA_HOST_PROF=1: the descent loop
+// prints it): where a latency-bound epoch (c1) spends the coordinator thread's time
+enum HostProfKey { kHpAsyncmap, kHpFlush, kHpPreConsume, kHpPrearm, kHpLaunch, kHpWaitany, kHpHarvest, kHpPost, kHpUpdate,
+                   kHpKeys };
+#if MPA_MEASURE
+struct HostProf {
+  std::atomic<int64_t> ns[kHpKeys];
+  std::atomic<int64_t> n[kHpKeys];
+};
+extern HostProf g_hprof;
+struct HostProfScope {
+  int k;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  ~HostProfScope() {
+    g_hprof.ns[k].fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(),
+                            std::memory_order_relaxed);
+    g_hprof.n[k].fetch_add(1, std::memory_order_relaxed);
+  }
+};
+#define MPA_HPROF(key) ::mpa::HostProfScope hprof_scope_{key}
+#else
+#define MPA_HPROF(key) (void)0
+#endif
+
 class HipComm final : public Comm {
  public:
   enum Role { SOLO, COORD, SERVER };

@@ -335,11 +335,15 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   P* __restrict__ slab = static_cast<P*>(a.slab);
   T* __restrict__ out = static_cast<T*>(a.out);
   const unsigned G = unsigned(a.grid);
+  // a reply that stays on this GPU is stored write-through (publish_done_wt needs no release)
   auto store_out = [&](int j, const P& s) {
     const int c0 = j * E;
 #pragma unroll
     for (int e = 0; e < E; ++e)
-      if (c0 + e < a.cols) out[c0 + e] = s.v[e];
+      if (c0 + e < a.cols) {
+        if (a.pub_local) st_agent(out + c0 + e, s.v[e]);
+        else out[c0 + e] = s.v[e];
+      }
   };
   bool cx = false;  // cancelled (read by the reply's writer only)
   // One-level tree for small partials (one 16-B vector per lane, <= 64 workgroups: c1's tasks):
@@ -454,7 +458,10 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   drain_vm();
   __syncthreads();
   if (cx) return;
-  if (tid == 0) publish_task(a.flag, a.seq, a.pub_local);
+  if (tid == 0) {
+    if (a.pub_local) publish_done_wt(a.flag, a.seq);
+    else publish_done(a.flag, a.seq);
+  }
   if (!batch.tail) return;
   // Fused tail: this workgroup finished its task (and published it); the last task of the
   // launch to finish runs the next epoch's coordinator step.  publish_done released the

@@ -27,6 +27,9 @@
 #include "hip_transport.hpp"
 
 namespace mpa {
+#if MPA_MEASURE
+HostProf g_hprof;
+#endif
 
 // rank 0 waits for remote completions of a launched-ahead epoch with one wait_words_kernel
 // (default) or, MPA_WAIT_VALUE_OPS=1 (measurement build), one hipStreamWaitValue64 per remote worker
@@ -235,6 +238,7 @@ void HipComm::check_buffers(const CallBufs& b) {
 }
 
 void HipComm::post(int64_t i, int64_t rank, int64_t tag) {
+  MPA_HPROF(kHpPost);
   (void)tag;
   if (shutdown_) fail(MPA_ERROR, "comm has been shut down");
   HipWorker& w = w_[size_t(rank - 1)];
@@ -271,6 +275,7 @@ void HipComm::post(int64_t i, int64_t rank, int64_t tag) {
 }
 
 void HipComm::harvest(int64_t i, int64_t rank) {
+  MPA_HPROF(kHpHarvest);
   HipWorker& w = w_[size_t(rank - 1)];
   if (int64_t* e = trace_entry(w)) e[kTHarvest] = int64_t(mono_ns());
   if (w.preharvest) {  // already in the epoch kernel enqueued ahead
@@ -281,6 +286,7 @@ void HipComm::harvest(int64_t i, int64_t rank) {
 }
 
 int64_t HipComm::waitany(int64_t n, const int64_t* ranks, const uint8_t* live) {
+  MPA_HPROF(kHpWaitany);
   bool any = false;
   for (int64_t i = 0; i < n; ++i) any |= live[i] != 0;
   if (!any) return -1;
@@ -314,6 +320,7 @@ void HipComm::waitall(int64_t n, const int64_t* ranks, const uint8_t* live) {
 }
 
 void HipComm::flush() {
+  MPA_HPROF(kHpFlush);
   if (pre_active_ && pre_consume()) return;  // the pre-armed launch runs this epoch
   if (defer_stale()) return;                 // held re-dispatches: nothing to launch yet
   cancel_pre();
@@ -374,6 +381,7 @@ void HipComm::flush() {
 // nwait < n (launch-ahead and the fused tail cover nwait = n), right after a fused-head launch
 // of the whole pool, and not for the one launch in `timing_period_` that the timing samples.
 void HipComm::maybe_prearm(int dtype) {
+  MPA_HPROF(kHpPrearm);
   if (!prearm_ || !prearm_loop_ || !defer_end_ || b_.await_all || gated() || role_ != SOLO || pre_active_ || !held_.empty())
     return;
   if (timing_ && timing_period_ > 1 && ++pre_count_ % timing_period_ == 0) {
@@ -413,6 +421,7 @@ void HipComm::maybe_prearm(int dtype) {
 // the same slots with the task numbers it carries, a fused-head step.  Its arguments go to
 // the mailbox, then the go word (release: the launch reads them after it).
 bool HipComm::pre_consume() {
+  MPA_HPROF(kHpPreConsume);
   const std::vector<int64_t> ranks = launch_ranks();
   if (!has_update_ || ranks != pre_ranks_ || hold_next_ || !fused_ok(upd_, posts_) || !head_fits(posts_, upd_) ||
       !deferred_fit(upd_))
