@@ -37,7 +37,10 @@
 //               presence cost the c2 launch 19 %)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #ifndef MPA_MEASURE
 #define MPA_MEASURE 0
@@ -115,6 +118,22 @@ struct Tile {
     }
   }
 };
+
+#if MPA_MEASURE
+// measurement build (MPA_HEAD_STAMP=1 dumps them): s_memrealtime of a fused-head launch, by its head
+// token: [0] workgroup 0 saw the go word, [1] it published the head token, [2] the first other
+// workgroup saw the token, [3] the first task's last reducer began its sum, [4] the last publish
+constexpr int kHeadSlots = 4096;
+__device__ unsigned long long g_head_stamp[kHeadSlots][5];
+__device__ __forceinline__ void head_stamp(uint32_t token, int k, bool first) {
+  unsigned long long* p = &g_head_stamp[token % kHeadSlots][k];
+  if (first) atomicMin(p, rt_now());
+  else atomicMax(p, rt_now());
+}
+#define MPA_HEAD_STAMP(tok, k, first) head_stamp(tok, k, first)
+#else
+#define MPA_HEAD_STAMP(tok, k, first) (void)0
+#endif
 
 template <typename T, int VPL, int RB, int MODE>
 __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
@@ -210,6 +229,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
           }
           if (v & kPreCancel) go = 0;
           else if (v & kPreSame) go = 2;
+          MPA_HEAD_STAMP(batch.head_token, 0, false);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the mailbox the host wrote
           s_go = go;
         }
@@ -235,7 +255,10 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       }
       drain_vm();
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(batch.head_word, batch.head_token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) {
+        __hip_atomic_store(batch.head_word, batch.head_token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        MPA_HEAD_STAMP(batch.head_token, 1, false);
+      }
     } else {
       if (base < hi) {
         t0.load(A, base, rows, a.lda, lane, vok);
@@ -248,7 +271,10 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
         // here beyond workgroup 0's (which publishes the cancel token on its timeout)
         for (unsigned k = 0;; ++k) {
           const uint32_t hw = __hip_atomic_load(batch.head_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (hw == batch.head_token) break;
+          if (hw == batch.head_token) {
+            MPA_HEAD_STAMP(batch.head_token, 2, true);
+            break;
+          }
           if (hw == (batch.head_token | kHeadCancel)) {
             s_ticket = 0;
             break;
@@ -362,6 +388,8 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     }
     __syncthreads();
     if (!s_ticket) return;
+    if constexpr ((MODE & M_HEAD) != 0)
+      if (tid == 0) MPA_HEAD_STAMP(batch.head_token, 3, true);
     cx = cancelled();
     const int j = tid & (S - 1), q = tid / S;  // kThreads = 4 * S: four partial sums per vector
     P acc;
@@ -459,6 +487,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   __syncthreads();
   if (cx) return;
   if (tid == 0) {
+    if constexpr ((MODE & M_HEAD) != 0) MPA_HEAD_STAMP(batch.head_token, 4, false);
     if (a.pub_local) publish_done_wt(a.flag, a.seq);
     else publish_done(a.flag, a.seq);
   }
@@ -642,6 +671,44 @@ static int v2048() {
 #endif
 
 const char* lsq_variant_name() { return kC2Variants[c2_variant()].name; }
+
+#if MPA_MEASURE
+void head_stamp_reset() {
+  static unsigned long long h[kHeadSlots][5];
+  for (int i = 0; i < kHeadSlots; ++i) {
+    h[i][0] = h[i][1] = h[i][3] = h[i][4] = 0;
+    h[i][2] = ~0ull;
+  }
+  h[0][3] = ~0ull;
+  for (int i = 0; i < kHeadSlots; ++i) h[i][3] = ~0ull;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_head_stamp), h, sizeof(h));
+}
+void head_stamp_dump() {
+  static unsigned long long h[kHeadSlots][5];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_head_stamp), sizeof(h)) != hipSuccess) return;
+  std::vector<double> d[6];
+  for (int i = 1; i < kHeadSlots; ++i) {
+    const auto* a = h[i];
+    const auto* p = h[i - 1];
+    if (!a[0] || !a[1] || a[2] == ~0ull || a[3] == ~0ull || !a[4]) continue;
+    d[0].push_back(double(a[1] - a[0]) / 100.0);  // 100 MHz realtime -> us
+    d[1].push_back(double(a[2] - a[1]) / 100.0);
+    d[2].push_back(double(a[3]) / 100.0 - double(a[2]) / 100.0);
+    d[3].push_back(double(a[4]) / 100.0 - double(a[3]) / 100.0);
+    d[4].push_back(double(a[4] - a[0]) / 100.0);
+    if (p[4] && p[4] < a[0]) d[5].push_back(double(a[0] - p[4]) / 100.0);  // previous publish -> this go
+  }
+  static const char* names[6] = {"go seen -> head token", "head token -> seen by another WG", "token seen -> first task's last reducer",
+                                 "last reducer -> last publish", "go seen -> last publish (device part)", "previous epoch's last publish -> go seen"};
+  std::fprintf(stderr, "[mpa head stamps] %zu launches (us, p10 / p50 / p90):\n", d[4].size());
+  for (int k = 0; k < 6; ++k) {
+    if (d[k].empty()) continue;
+    std::sort(d[k].begin(), d[k].end());
+    const size_t n = d[k].size();
+    std::fprintf(stderr, "  %-44s %6.2f %6.2f %6.2f\n", names[k], d[k][n / 10], d[k][n / 2], d[k][n * 9 / 10]);
+  }
+}
+#endif
 
 int lsq_set_variant(int i) {
   if (i < 0 || i >= kNumC2Variants) return -1;

@@ -157,6 +157,9 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   hold_ok_ = !env_off("MPA_HOLD");
   { const char* e = measure_env("MPA_GATHER"); batch_gather_ = !(e && *e == '0'); }
   if (const char* e = measure_env("MPA_LSQP_PF")) lsqp_pfd_ = std::max(0, std::min(8, std::atoi(e)));
+#if MPA_MEASURE
+  if (const char* hs = measure_env("MPA_HEAD_STAMP"); hs && *hs == '1') head_stamp_reset();
+#endif
   const char* dbg = std::getenv("MPA_DEBUG");
   debug_ = dbg && *dbg == '1';
   if (debug_ && region_) {
@@ -178,6 +181,7 @@ HipComm::~HipComm() {
 #if MPA_MEASURE
   if (const char* d = measure_env("MPA_LSQF_DBG"); d && (std::atoi(d) & 16)) lsqf_prof_dump();
   if (const char* d = measure_env("MPA_LSQP4_CLOCK"); d && *d == '1') lsqp4_clock_dump();
+  if (const char* d = measure_env("MPA_HEAD_STAMP"); d && *d == '1') head_stamp_dump();
 #endif
   for (auto& w : w_) {
     if (w.slab) (void)hipFree(w.slab);
