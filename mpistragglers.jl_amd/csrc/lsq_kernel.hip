@@ -214,6 +214,12 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
         // arguments then come from the pinned mailbox (one pass of 16-B reads into LDS)
         __shared__ EpochArgs s_ep;
         __shared__ int s_go;
+        // the launch's own arguments into LDS while the host decides: when its prediction holds
+        // (kPreSame, most epochs) the step starts the moment the go word lands
+        constexpr int kEpVecs = int(sizeof(EpochArgs) / 16);
+        static_assert(sizeof(EpochArgs) % 16 == 0, "EpochArgs copies in 16-B vectors");
+        for (int k = tid; k < kEpVecs; k += kThreads)
+          reinterpret_cast<uint4*>(&s_ep)[k] = reinterpret_cast<const uint4*>(&batch.ep)[k];
         if (tid == 0) {
           const unsigned long long t0s = rt_now();
           int go = 1;
@@ -239,13 +245,12 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
             __hip_atomic_store(batch.head_word, batch.head_token | kHeadCancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return;
         }
-        // the arguments into LDS: from the mailbox over the bus, or (s_go == 2: the host's
-        // prediction held) from the kernel arguments it was launched with
-        constexpr int kEpVecs = int(sizeof(EpochArgs) / 16);
-        static_assert(sizeof(EpochArgs) % 16 == 0, "EpochArgs copies in 16-B vectors");
-        const uint4* src = s_go == 2 ? reinterpret_cast<const uint4*>(&batch.ep) : reinterpret_cast<const uint4*>(batch.pre_ep);
-        for (int k = tid; k < kEpVecs; k += kThreads) reinterpret_cast<uint4*>(&s_ep)[k] = src[k];
-        __syncthreads();
+        // a changed decision: the arguments from the mailbox over the bus
+        if (s_go == 1) {
+          const uint4* src = reinterpret_cast<const uint4*>(batch.pre_ep);
+          for (int k = tid; k < kEpVecs; k += kThreads) reinterpret_cast<uint4*>(&s_ep)[k] = src[k];
+          __syncthreads();
+        }
         if ((batch.head & 3) == 2) epoch_elems<T, E, true, false>(s_ep, tid, kThreads);
         else epoch_elems<T, 1, true, false>(s_ep, tid, kThreads);
       } else if ((batch.head & 3) == 2) {
