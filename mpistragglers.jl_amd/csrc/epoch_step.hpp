@@ -28,41 +28,58 @@ template <typename T, int V>
 struct EVec {
   T v[V];
 };
+
+// Every pointer the step touches is global memory (this GPU's, a peer's or pinned host memory),
+// and its loads and stores go through address space 1 as global_* instructions.  Generic (flat)
+// ones also count against lgkmcnt and may alias LDS: with the pre-armed head's arguments staged
+// in LDS the compiler re-read each argument after every flat store and waited for every flat load
+// before it (c1's head step paid a memory round trip per chunk).
+#define MPA_GLOBAL __attribute__((address_space(1)))
+typedef unsigned SysU4 __attribute__((ext_vector_type(4)));
+typedef unsigned SysU2 __attribute__((ext_vector_type(2)));
+template <typename U>
+__device__ __forceinline__ U gld(const void* p) {
+  return *(const MPA_GLOBAL U*)p;
+}
+template <typename U>
+__device__ __forceinline__ void gst(void* p, U v) {
+  *(MPA_GLOBAL U*)p = v;
+}
+
 template <typename T, int V>
 __device__ __forceinline__ EVec<T, V> eld(const T* p) {
   if constexpr (V * sizeof(T) == 16) {
-    return __builtin_bit_cast(EVec<T, V>, *reinterpret_cast<const uint4*>(p));
+    return __builtin_bit_cast(EVec<T, V>, gld<SysU4>(p));
   } else if constexpr (V * sizeof(T) == 8 && V > 1) {
-    return __builtin_bit_cast(EVec<T, V>, *reinterpret_cast<const uint2*>(p));
+    return __builtin_bit_cast(EVec<T, V>, gld<SysU2>(p));
   } else if constexpr (V * sizeof(T) == 32) {
     struct U2 {
-      uint4 a, b;
+      SysU4 a, b;
     };
-    const uint4* q = reinterpret_cast<const uint4*>(p);
-    return __builtin_bit_cast(EVec<T, V>, (U2{q[0], q[1]}));
+    return __builtin_bit_cast(EVec<T, V>, (U2{gld<SysU4>(p), gld<SysU4>(reinterpret_cast<const SysU4*>(p) + 1)}));
   } else {
     EVec<T, V> r;
 #pragma unroll
-    for (int e = 0; e < V; ++e) r.v[e] = p[e];
+    for (int e = 0; e < V; ++e) r.v[e] = gld<T>(p + e);
     return r;
   }
 }
 template <typename T, int V>
 __device__ __forceinline__ void est(T* p, const EVec<T, V>& v) {
   if constexpr (V * sizeof(T) == 16) {
-    *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, v);
+    gst<SysU4>(p, __builtin_bit_cast(SysU4, v));
   } else if constexpr (V * sizeof(T) == 8 && V > 1) {
-    *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, v);
+    gst<SysU2>(p, __builtin_bit_cast(SysU2, v));
   } else if constexpr (V * sizeof(T) == 32) {
     struct U2 {
-      uint4 a, b;
+      SysU4 a, b;
     };
     const U2 u = __builtin_bit_cast(U2, v);
-    reinterpret_cast<uint4*>(p)[0] = u.a;
-    reinterpret_cast<uint4*>(p)[1] = u.b;
+    gst<SysU4>(p, u.a);
+    gst<SysU4>(reinterpret_cast<SysU4*>(p) + 1, u.b);
   } else {
 #pragma unroll
-    for (int e = 0; e < V; ++e) p[e] = v.v[e];
+    for (int e = 0; e < V; ++e) gst<T>(p + e, v.v[e]);
   }
 }
 
@@ -75,28 +92,28 @@ using H16 = EVec<uint16_t, V>;
 template <int V>
 __device__ __forceinline__ void st_bf16(uint16_t* p, const H16<V> h) {
   if constexpr (V == 8) {
-    *reinterpret_cast<uint4*>(p) = __builtin_bit_cast(uint4, h);
+    gst<SysU4>(p, __builtin_bit_cast(SysU4, h));
   } else if constexpr (V == 4) {
-    *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, h);
+    gst<SysU2>(p, __builtin_bit_cast(SysU2, h));
   } else if constexpr (V == 2) {
-    *reinterpret_cast<unsigned*>(p) = __builtin_bit_cast(unsigned, h);
+    gst<unsigned>(p, __builtin_bit_cast(unsigned, h));
   } else {
 #pragma unroll
-    for (int e = 0; e < V; ++e) p[e] = h.v[e];
+    for (int e = 0; e < V; ++e) gst<uint16_t>(p + e, h.v[e]);
   }
 }
 template <int V>
 __device__ __forceinline__ H16<V> ld_bf16(const uint16_t* p) {
   if constexpr (V == 8) {
-    return __builtin_bit_cast(H16<V>, *reinterpret_cast<const uint4*>(p));
+    return __builtin_bit_cast(H16<V>, gld<SysU4>(p));
   } else if constexpr (V == 4) {
-    return __builtin_bit_cast(H16<V>, *reinterpret_cast<const uint2*>(p));
+    return __builtin_bit_cast(H16<V>, gld<SysU2>(p));
   } else if constexpr (V == 2) {
-    return __builtin_bit_cast(H16<V>, *reinterpret_cast<const unsigned*>(p));
+    return __builtin_bit_cast(H16<V>, gld<unsigned>(p));
   } else {
     H16<V> h;
 #pragma unroll
-    for (int e = 0; e < V; ++e) h.v[e] = p[e];
+    for (int e = 0; e < V; ++e) h.v[e] = gld<uint16_t>(p + e);
     return h;
   }
 }
@@ -106,8 +123,6 @@ __device__ __forceinline__ H16<V> ld_bf16(const uint16_t* p) {
 // them (s_waitcnt vmcnt(0)) they are visible at system scope, so the doorbell behind them needs
 // no L2 writeback: a system-scope release fence in every workgroup wrote back each XCD's whole
 // L2 (the recvbuf, x and mirror stores of the step too) before the doorbells could ring.
-typedef unsigned SysU4 __attribute__((ext_vector_type(4)));
-typedef unsigned SysU2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st_sys(void* p, uint4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(__builtin_bit_cast(SysU4, v)) : "memory");
 }
@@ -157,12 +172,12 @@ __device__ __forceinline__ void st_bf16_sys(uint16_t* p, const H16<V> h) {
 template <typename T>
 __device__ __forceinline__ void st_agent(T* p, T v) {
   using U = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned>::type;
-  __hip_atomic_store(reinterpret_cast<U*>(p), __builtin_bit_cast(U, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((MPA_GLOBAL U*)p, __builtin_bit_cast(U, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
   using U = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned>::type;
-  return __builtin_bit_cast(T, __hip_atomic_load(reinterpret_cast<const U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return __builtin_bit_cast(T, __hip_atomic_load((const MPA_GLOBAL U*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 // Vectors jv = first, first + stride, ... of V elements (16-B vectors when every pointer

@@ -122,9 +122,10 @@ struct Tile {
 #if MPA_MEASURE
 // measurement build (MPA_HEAD_STAMP=1 dumps them): s_memrealtime of a fused-head launch, by its head
 // token: [0] workgroup 0 saw the go word, [1] it published the head token, [2] the first other
-// workgroup saw the token, [3] the first task's last reducer began its sum, [4] the last publish
+// workgroup saw the token, [3] the first task's last reducer began its sum, [4] the last publish,
+// [5] workgroup 0 starts the step (after the acquire and its arguments), [6] the step's stores issued
 constexpr int kHeadSlots = 4096;
-__device__ unsigned long long g_head_stamp[kHeadSlots][5];
+__device__ unsigned long long g_head_stamp[kHeadSlots][7];
 __device__ __forceinline__ void head_stamp(uint32_t token, int k, bool first) {
   unsigned long long* p = &g_head_stamp[token % kHeadSlots][k];
   if (first) atomicMin(p, rt_now());
@@ -679,9 +680,9 @@ const char* lsq_variant_name() { return kC2Variants[c2_variant()].name; }
 
 #if MPA_MEASURE
 void head_stamp_reset() {
-  static unsigned long long h[kHeadSlots][5];
+  static unsigned long long h[kHeadSlots][7];
   for (int i = 0; i < kHeadSlots; ++i) {
-    h[i][0] = h[i][1] = h[i][3] = h[i][4] = 0;
+    h[i][0] = h[i][1] = h[i][3] = h[i][4] = h[i][5] = h[i][6] = 0;
     h[i][2] = ~0ull;
   }
   h[0][3] = ~0ull;
@@ -689,9 +690,9 @@ void head_stamp_reset() {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_head_stamp), h, sizeof(h));
 }
 void head_stamp_dump() {
-  static unsigned long long h[kHeadSlots][5];
+  static unsigned long long h[kHeadSlots][7];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_head_stamp), sizeof(h)) != hipSuccess) return;
-  std::vector<double> d[6];
+  std::vector<double> d[9];
   for (int i = 1; i < kHeadSlots; ++i) {
     const auto* a = h[i];
     const auto* p = h[i - 1];
@@ -702,11 +703,17 @@ void head_stamp_dump() {
     d[3].push_back(double(a[4]) / 100.0 - double(a[3]) / 100.0);
     d[4].push_back(double(a[4] - a[0]) / 100.0);
     if (p[4] && p[4] < a[0]) d[5].push_back(double(a[0] - p[4]) / 100.0);  // previous publish -> this go
+    if (a[5] && a[6] && a[5] >= a[0] && a[6] >= a[5] && a[1] >= a[6]) {  // the pre-armed head's step, split
+      d[6].push_back(double(a[5] - a[0]) / 100.0);
+      d[7].push_back(double(a[6] - a[5]) / 100.0);
+      d[8].push_back(double(a[1] - a[6]) / 100.0);
+    }
   }
-  static const char* names[6] = {"go seen -> head token", "head token -> seen by another WG", "token seen -> first task's last reducer",
-                                 "last reducer -> last publish", "go seen -> last publish (device part)", "previous epoch's last publish -> go seen"};
+  static const char* names[9] = {"go seen -> head token", "head token -> seen by another WG", "token seen -> first task's last reducer",
+                                 "last reducer -> last publish", "go seen -> last publish (device part)", "previous epoch's last publish -> go seen",
+                                 "  go seen -> step start (acquire, arguments)", "  step start -> step's stores issued", "  stores issued -> head token (drain)"};
   std::fprintf(stderr, "[mpa head stamps] %zu launches (us, p10 / p50 / p90):\n", d[4].size());
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < 9; ++k) {
     if (d[k].empty()) continue;
     std::sort(d[k].begin(), d[k].end());
     const size_t n = d[k].size();
