@@ -192,13 +192,18 @@ __device__ __forceinline__ void epoch_elems(const EpochArgs& a, int64_t first, i
   T* recv = reinterpret_cast<T*>(a.recv);
   T* x = static_cast<T*>(a.x);
   const int64_t nv = a.elems / V;
+  // chunks past n load from pad: x's address, hidden from the compiler -- a load it could
+  // identify with the iterate's own it replaced by a copy of that value, which waited for the
+  // iterate's load before the chunks' loads were issued (two memory round trips, not one)
+  const T* pad = x;
+  asm volatile("" : "+v"(pad));
   for (int64_t jv = first; jv < nv; jv += stride) {
     const int64_t j = jv * V;
     EVec<T, V> v = eld<T, V>(x + j);
     EVec<T, V> c[kMaxEpochChunks];
 #pragma unroll
     for (int i = 0; i < kMaxEpochChunks; ++i) {
-      const T* src = i < a.n ? (a.hsrc[i] ? reinterpret_cast<const T*>(a.hsrc[i]) : recv + int64_t(i) * a.elems) : x;
+      const T* src = i < a.n ? (a.hsrc[i] ? reinterpret_cast<const T*>(a.hsrc[i]) : recv + int64_t(i) * a.elems) : pad;
       c[i] = eld<T, V>(src + j);
     }
 #pragma unroll

@@ -252,8 +252,10 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
           for (int k = tid; k < kEpVecs; k += kThreads) reinterpret_cast<uint4*>(&s_ep)[k] = src[k];
           __syncthreads();
         }
+        if (tid == 0) MPA_HEAD_STAMP(batch.head_token, 5, false);
         if ((batch.head & 3) == 2) epoch_elems<T, E, true, false>(s_ep, tid, kThreads);
         else epoch_elems<T, 1, true, false>(s_ep, tid, kThreads);
+        if (tid == 0) MPA_HEAD_STAMP(batch.head_token, 6, false);
       } else if ((batch.head & 3) == 2) {
         epoch_elems<T, E, true, false>(batch.ep, tid, kThreads);
       } else {
@@ -703,16 +705,16 @@ void head_stamp_dump() {
     d[3].push_back(double(a[4]) / 100.0 - double(a[3]) / 100.0);
     d[4].push_back(double(a[4] - a[0]) / 100.0);
     if (p[4] && p[4] < a[0]) d[5].push_back(double(a[0] - p[4]) / 100.0);  // previous publish -> this go
-    if (a[5] && a[6] && a[5] >= a[0] && a[6] >= a[5] && a[1] >= a[6]) {  // the pre-armed head's step, split
-      d[6].push_back(double(a[5] - a[0]) / 100.0);
-      d[7].push_back(double(a[6] - a[5]) / 100.0);
-      d[8].push_back(double(a[1] - a[6]) / 100.0);
+    if (a[5] && a[6]) {  // the pre-armed head's step, split
+      d[6].push_back(double(a[5]) / 100.0 - double(a[0]) / 100.0);
+      d[7].push_back(double(a[6]) / 100.0 - double(a[5]) / 100.0);
+      d[8].push_back(double(a[1]) / 100.0 - double(a[6]) / 100.0);
     }
   }
   static const char* names[9] = {"go seen -> head token", "head token -> seen by another WG", "token seen -> first task's last reducer",
                                  "last reducer -> last publish", "go seen -> last publish (device part)", "previous epoch's last publish -> go seen",
                                  "  go seen -> step start (acquire, arguments)", "  step start -> step's stores issued", "  stores issued -> head token (drain)"};
-  std::fprintf(stderr, "[mpa head stamps] %zu launches (us, p10 / p50 / p90):\n", d[4].size());
+  std::fprintf(stderr, "[mpa head stamps] %zu launches, %zu with the step split (us, p10 / p50 / p90):\n", d[4].size(), d[6].size());
   for (int k = 0; k < 9; ++k) {
     if (d[k].empty()) continue;
     std::sort(d[k].begin(), d[k].end());
