@@ -64,6 +64,14 @@ struct Tile {
   using P = Pack<T>;
   static constexpr int E = P::E;
   P d[RB][VPL];
+  // the fp64 fused-head variant's b values, loaded with the tile (load_b): under the head's
+  // control flow each row's b load was issued in its own branch and waited for there, one memory
+  // round trip per row (c1's 16-row tiles: most of its tasks' time); clamped, they issue together,
+  // before the token wait for a prefetched tile.  fp32 keeps the per-row loads: there the moved
+  // loads changed how the compiler contracted the row's update, and the head variant no longer
+  // matched the plain one bit for bit (r05bf)
+  static constexpr bool kHeadB = (MODE & M_HEAD) != 0 && sizeof(T) == 8;
+  [[maybe_unused]] T bq[kHeadB ? RB : 1];
 
   // rows [base, base+RB): out-of-range rows/vectors either branch (default) or read a
   // clamped in-bounds address (M_CLAMP: the row's last valid row, vector 0 of the row for
@@ -93,6 +101,16 @@ struct Tile {
     }
   }
 
+  __device__ __forceinline__ void load_b(const T* __restrict__ bv, int64_t base, int64_t rows) {
+    if constexpr (kHeadB) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const int64_t r = base + rb;
+        bq[rb] = bv[r < rows ? r : rows - 1];
+      }
+    }
+  }
+
   __device__ __forceinline__ void compute(const T* __restrict__ bv, int64_t base, int64_t rows, const P (&xr)[VPL],
                                           P (&g)[VPL]) const {
     T dot[RB];
@@ -110,7 +128,9 @@ struct Tile {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       const int64_t r = base + rb;
-      const T res = (r < rows) ? dot[rb] - bv[r] : T(0);
+      T res;
+      if constexpr (kHeadB) res = (r < rows) ? dot[rb] - bq[rb] : T(0);
+      else res = (r < rows) ? dot[rb] - bv[r] : T(0);
 #pragma unroll
       for (int v = 0; v < VPL; ++v)
 #pragma unroll
@@ -270,6 +290,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     } else {
       if (base < hi) {
         t0.load(A, base, rows, a.lda, lane, vok);
+        t0.load_b(bv, base, rows);
         pre = true;
       }
       if (tid == 0) {
@@ -324,7 +345,10 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     }
   } else if constexpr ((MODE & M_HEAD) != 0) {
     for (; base < hi; base += step) {
-      if (!pre) t0.load(A, base, rows, a.lda, lane, vok);
+      if (!pre) {
+        t0.load(A, base, rows, a.lda, lane, vok);
+        t0.load_b(bv, base, rows);
+      }
       pre = false;
       t0.compute(bv, base, rows, xr, g);
     }
