@@ -422,15 +422,21 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     if (!s_ticket) return;
     if constexpr ((MODE & M_HEAD) != 0)
       if (tid == 0) MPA_HEAD_STAMP(batch.head_token, 3, true);
-    cx = cancelled();
     const int j = tid & (S - 1), q = tid / S;  // kThreads = 4 * S: four partial sums per vector
     P acc;
 #pragma unroll
     for (int e = 0; e < E; ++e) acc.v[e] = T(0);
+    // clamped, every load issues at once (each one under its own branch was waited for there:
+    // up to 16 round trips in a row for the last reducer of a 64-workgroup task)
     P t[16];
 #pragma unroll
-    for (int m = 0; m < 16; ++m)
-      if (q + 4 * m < int(G)) t[m] = ld_sc1(&slab[size_t(q + 4 * m) * S + j]);
+    for (int m = 0; m < 16; ++m) {
+      const int p = q + 4 * m < int(G) ? q + 4 * m : int(G) - 1;
+      t[m] = ld_sc1(&slab[size_t(p) * S + j]);
+    }
+    // the cancel word (pinned host memory: a PCIe round trip) read while the partials' loads are
+    // in flight, not before they issue
+    cx = cancelled();
 #pragma unroll
     for (int m = 0; m < 16; ++m)
       if (q + 4 * m < int(G))
