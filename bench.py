@@ -67,6 +67,20 @@ CONFIGS = {
                desc="BASELINE configs[4] shape: batched 64-iterate variant, bf16 A 2^23x2048 "
                     "(4 GiB per worker), X 2048x64, fp32 accumulate (MFMA), nwait=7"),
 }
+# measurement shapes, not bench lines: ONE GPU's share of the node's run,
+# i.e. the launch each GPU runs per epoch at N = 2 / 4 / 8 (8/N of the 8 workers of the same
+# global problem, one batched launch of their tasks), nwait = n and no delays, so the line is
+# that launch's own roofline and the denominator of DESIGN.md §5's scaling budget
+for _base, _ns in (("c2", (2, 4, 8)), ("c3", (8,)), ("c4", (8,)), ("c5", (8,))):
+    for _n in _ns:
+        _c = dict(CONFIGS[_base])
+        _w = 8 // _n
+        _c.update(rows=_c["rows"] // _n, workers=_w, nwait=_w, timing_period=1)
+        for _k in ("delay_mean_ms", "stale_weight"):
+            _c.pop(_k, None)
+        _c["desc"] = ("measurement: one GPU's share of %s at N = %d (%d task(s) of %d rows x %d %s per launch, "
+                      "nwait = n, no delays)" % (_base, _n, _w, _c["rows"] // _w, _c["cols"], _c["dtype"]))
+        CONFIGS["%sn%d" % (_base, _n)] = _c
 
 
 def parse():

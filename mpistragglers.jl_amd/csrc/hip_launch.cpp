@@ -470,6 +470,7 @@ void HipComm::launch_lsq_batch(const std::vector<int64_t>& ranks, int dtype, hip
 LsqBatch HipComm::build_lsq_batch(const std::vector<int64_t>& ranks, int dtype, double* bytes_out, int share) {
   LsqBatch b{};
   b.ntasks = int(ranks.size());
+  b.alone = here_count_ == 1 ? 1 : 0;
   const int split = share > b.ntasks ? share : b.ntasks;
   b.err = err_dev_;
   b.spin_ticks = spin_ticks();

@@ -289,10 +289,28 @@ class HipComm final : public Comm {
   // epoch's batched launch instead of alone before it (c5, nwait 7 of 8: one 8-task launch
   // per epoch instead of a 1-task launch and a 7-task launch, profiles/r02_c5_hold_ab.txt).
   // The pool's state machine is unchanged; MPA_HOLD=0 launches re-dispatches at once.
+  // Only while another task of this process is still running does holding pay: with nothing
+  // local in flight (rank 0 of the node's placement, whose one local worker is the stale one)
+  // the held task would only start one epoch late, so it launches at once (r06b).
   void flush_stale() override {
-    hold_next_ = hold_ok_;
+    hold_next_ = hold_ok_ && local_in_flight();
     flush();
     hold_next_ = false;
+  }
+  // a local undelayed least-squares worker (its tasks run in the batches a held task joins)
+  // other than the ones this flush posts has a launched task not yet seen done
+  bool local_in_flight() const {
+    for (int64_t r = 1; r <= nworkers_; ++r) {
+      const HipWorker& w = w_[size_t(r - 1)];
+      const TaskSpec& ts = tasks_[size_t(r - 1)];
+      if (!w.here || w.remote || w.seq == 0 || !ts.delays_ns.empty() ||
+          (ts.kind != MPA_TASK_LSQ && ts.kind != MPA_TASK_LSQ_BATCH) || done(r))
+        continue;
+      if (std::find(posts_.begin(), posts_.end(), r) != posts_.end()) continue;
+      if (std::find(held_.begin(), held_.end(), r) != held_.end()) continue;
+      return true;
+    }
+    return false;
   }
   void set_wait_hold(bool may_hold) override { may_hold_ = may_hold; }
   void release_held();
@@ -748,6 +766,7 @@ class HipComm final : public Comm {
   // ran in it (off: batches share the coordinator stream, so a partial grid idles CUs; c5
   // 19.9 vs 11.1 ms per epoch, profiles/r02_c5_lsqp_tuning.txt)
   bool lsqp_share_ = false;
+  int here_count_ = 0;       // workers this process serves
   bool hold_ok_ = true;     // MPA_HOLD=0: a stale re-dispatch launches at once (flush_stale)
   bool hold_next_ = false;  // set while flush_stale() flushes
   bool may_hold_ = false;   // this call's wait completes without the held tasks (set_wait_hold)

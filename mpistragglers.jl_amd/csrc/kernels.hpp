@@ -131,7 +131,11 @@ constexpr unsigned long long kCancelBit = 1ull << 62;
 
 // Reduction tree of a least-squares task (lsq_kernel.hip): fan-in, most workgroups per
 // task, and the counters it needs (level l has ceil(kLsqMaxGrid / 8^(l+1)) groups).
-constexpr int kLsqFanIn = 8;
+#ifndef MPA_LSQ_FANIN
+#define MPA_LSQ_FANIN 8  // (a measurement library may be built with another: make DEFS=-DMPA_LSQ_FANIN=16)
+#endif
+constexpr int kLsqFanIn = MPA_LSQ_FANIN;
+static_assert(kLsqFanIn >= 4 && kLsqFanIn <= 16, "tree fan-in");
 constexpr int kLsqMaxGrid = 1024;
 constexpr int kLsqCtrPerTask = 160;  // 128 + 16 + 2 + 1, rounded up
 
@@ -144,6 +148,10 @@ constexpr unsigned long long kPreCancel = 1ull << 63;
 constexpr unsigned long long kPreSame = 1ull << 62;  // the step's arguments are `ep` as launched
 struct LsqBatch {
   int ntasks;
+  // 1: the process serves this one worker only (the node's placement at N = 8), so the launch
+  // never shares the GPU with another task launch of its own: a lone 2048-column fp32 task then
+  // takes the batched launch's 32 KiB tile (c3n8 0.76 -> 0.88 of HBM, profiles/r06_pergpu.txt)
+  int alone;
   unsigned* err;
   unsigned long long spin_ticks;
   int block0[kMaxLsqTasks + 1];

@@ -781,10 +781,12 @@ hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s) {
 #endif
         // a batched launch of several tasks (one grid for all of them: nwait = n, no delays)
         // streams 32 KiB per wave and tile: the c3 tasks batched (measurement config c3k) 0.76
-        // -> 0.83-0.90 of HBM; one task per launch (c3's delayed tasks, two to four launches
+        // -> 0.83-0.90 of HBM, and so does a lone task of a process that serves one worker (the
+        // node's N = 8 placement, measurement config c3n8: 0.76 -> 0.88, profiles/r06_pergpu.txt);
+        // one task per launch beside others (c3's delayed tasks at N = 1, two to four launches
         // overlapping) keeps 16 KiB and three waves per SIMD: -4 % with four rows
         // (profiles/r05_lsq2048.txt)
-        if (a.ntasks >= 2) return go<float, 8, 4, kMode>(a, s);
+        if (a.ntasks >= 2 || a.alone) return go<float, 8, 4, kMode>(a, s);
         return go<float, 8, 2, kMode>(a, s);
       default: return hipErrorInvalidValue;
     }

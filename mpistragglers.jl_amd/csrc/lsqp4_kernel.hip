@@ -73,7 +73,16 @@ constexpr int NCT = QKW / 16;         // column tiles of phase 2 (32)
 constexpr int PH = 32;                // iterates per workgroup (one half)
 constexpr int SLICE = PRB * ROWB;     // 16 KiB
 constexpr int XS = PH * 2 + 16;       // X staging row stride (bytes)
-constexpr int PF = 4;                 // G tree fan-in
+#ifndef MPA_LSQP4_PF
+#define MPA_LSQP4_PF 4                // G tree fan-in
+#endif
+constexpr int PF = MPA_LSQP4_PF;
+static_assert(PF >= 2 && PF <= 8, "tree fan-in");
+#ifndef MPA_LSQP4_TJB
+#define MPA_LSQP4_TJB 8               // G tree: column tiles per round of loads (x PF members in flight)
+#endif
+constexpr int kTreeJB = MPA_LSQP4_TJB;
+static_assert((2 * 32) % kTreeJB == 0, "tiles per round");
 #ifndef MPA_LSQP4_P2L
 #define MPA_LSQP4_P2L 1               // phase-2 transposed-read chunks in flight ahead (1 vs 2: -1 %, r02_c5_strip_ring.txt)
 #endif
@@ -697,15 +706,34 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       const unsigned next = (count + PF - 1) / PF;
       if (next == 1) cx = disarmed(a.go, a.seq);
       const f32x4* src = slab + size_t(first) * stride * qstride;
-#pragma unroll 4
-      for (int j2 = 0; j2 < 2 * NCT; ++j2) {
-        const int j = j2 * 64 + lane;
-        f32x4 s = ld_wt(src + j);
-        for (unsigned m = 1; m < gsize; ++m) s += ld_wt(src + size_t(m) * stride * qstride + j);
-        if (next == 1) {
-          if (!cx) store_out(j2 / NCT, j2 % NCT, s);
-        } else {
-          st_wt(slab + size_t(first) * stride * qstride + j, s);
+      // JB tiles x PF members of loads in flight at once (clamped to member 0 past the group,
+      // their sums selected away): one wave reduces its 64 KiB slice of the group, and with
+      // one load chain per tile (each member's load waited for before the next issued) a
+      // single-task launch spent ~0.2 ms in its four tree levels (c5n8, profiles/r06_pergpu.txt).
+      // Summed in member order as before, so the result is bitwise the same.
+#pragma unroll 1
+      for (int jb = 0; jb < 2 * NCT; jb += kTreeJB) {
+        f32x4 v[PF][kTreeJB];
+#pragma unroll
+        for (int m = 0; m < PF; ++m) {
+          const size_t mo = size_t(unsigned(m) < gsize ? m : 0) * stride * qstride;
+#pragma unroll
+          for (int jj = 0; jj < kTreeJB; ++jj) v[m][jj] = ld_wt(src + mo + (jb + jj) * 64 + lane);
+        }
+#pragma unroll
+        for (int jj = 0; jj < kTreeJB; ++jj) {
+          f32x4 s = v[0][jj];
+#pragma unroll
+          for (int m = 1; m < PF; ++m) {
+            const f32x4 t = s + v[m][jj];
+            if (unsigned(m) < gsize) s = t;
+          }
+          const int j2 = jb + jj;
+          if (next == 1) {
+            if (!cx) store_out(j2 / NCT, j2 % NCT, s);
+          } else {
+            st_wt(slab + size_t(first) * stride * qstride + j2 * 64 + lane, s);
+          }
         }
       }
       if (next == 1) break;

@@ -102,6 +102,7 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   // front (the round-1 behaviour, for A/B measurements).
   int here_count = 0;
   for (const auto& w : w_) here_count += w.here;
+  here_count_ = here_count;
   const char* eager = measure_env("MPA_EAGER_STREAMS");
   if (eager && *eager == '1') {
     for (auto& w : w_)

@@ -547,6 +547,220 @@ def lsq_sched_dist(rank, world, port, placement, config, epoch0, result_q):
         raise
 
 
+# The native k-of-n loop across processes: what bench.py's rank 0 runs at
+# N > 1 for c3 / c4 / c5 (make_loop: mpa_lsq_descent / mpa_lsqb_descent on a DistComm).  Worker 1
+# lives on rank 0; `rows` makes it the slow one (an undelayed local task: its stale reply and its
+# re-dispatch, src/MPIAsyncPools.jl:177-184), the remote workers carry Exp(delay_ms) injected
+# delays (their stale replies are harvested from other processes' GPUs).
+KOFN_CONFIGS = {
+    # c3: fp32, nwait 6 of 8, stale results dropped; the node's placement (rank 0 serves worker
+    # 1 only), so worker 1's stale re-dispatch launches at once (nothing else of rank 0's runs)
+    "c3": dict(dt="f32", cols=2048, nwait=6, stale=0.0, tol=1e-5, placement=list(range(8)),
+               rows=[1 << 19] + [256] * 7, delay_ms=0.1, epochs=40, eta=0.005),
+    # c4: fp64, worker 1 fresh + 5 others (first_plus), stale results at weight 0.5; worker 1 fast
+    "c4": dict(dt="f64", cols=2048, nwait="first_plus5", stale=0.5, tol=1e-12, placement=list(range(8)),
+               rows=[256] * 8, delay_ms=1.0, epochs=40, eta=0.05),
+    # c5: the batched 64-iterate variant (bf16 messages, fp32 accumulate), nwait 7 of 8; rank 0
+    # serves workers 1 and 2 (worker 2's task queues behind worker 1's on the coordinator
+    # stream), so worker 1's stale re-dispatch is HELD and joins worker 2's next launch; eta
+    # small enough that G never cancels down to its rounding (bf16 messages)
+    "c5": dict(dt="bf16", cols=2048, nwait=7, stale=0.0, tol=1e-5, placement=[0, 0, 1, 2, 3, 4, 5, 6],
+               rows=[1 << 18, 1 << 16] + [256] * 6, delay_ms=0.1, epochs=30, eta=1e-4, k=64),
+}
+
+
+def descent_kofn_dist(rank, world, port, config, epoch0, result_q):
+    """BASELINE c3 / c4 / c5's coordinator loop in native code (M.lsq_descent / M.lsqb_descent,
+    as bench.py runs it at N > 1) on rank 0 of a DistComm (the node's placement, rank 0 serving
+    worker 1 and ranks 1-7 one worker each; c5: rank 0 serving workers 1 and 2), ungated, at
+    nwait < n.  Whatever the timing, the loop
+    must compute what the reference's coordinator computes from the repochs it saw
+    (examples/iterative_example.jl:41-46): rank 0 traces the per-epoch repochs
+    (MPA_DESCENT_TRACE=1) and replays them in torch fp64 on the device -- each chunk i the
+    gradient of the iterate sent at its repochs[i] (c5: the bf16 rounding of that iterate),
+    weights fresh 1 / stale `stale` / never heard from 0, scaled by n / sum(w) -- and the final
+    iterate must match the replay (1e-5 fp32 and bf16-in/fp32-accumulate, 1e-12 fp64); every
+    final chunk is the gradient of the iterate sent at its repochs (after waitall!); the paths
+    the node's run depends on did run: remote stale harvests, stale harvests of the slow local
+    worker (c3, c5), its re-dispatch launched at once where nothing else of rank 0's runs (c3: no
+    hold) and held into worker 2's next launch where it would queue behind it (c5), the
+    first_plus predicate on remote completions (c4)."""
+    import re
+    import tempfile
+    import numpy as np
+    try:
+        dist = _init(rank, world, port)
+        import torch
+        torch.cuda.set_device(0)
+        import mpiasyncpools as M
+        cfg = KOFN_CONFIGS[config]
+        placement, cols, k = cfg["placement"], cfg["cols"], cfg.get("k", 1)
+        n = len(placement)
+        assert world == max(placement) + 1, (world, placement)
+        tdt = {"f32": torch.float32, "f64": torch.float64, "bf16": torch.bfloat16}[cfg["dt"]]
+        es = {"f32": 4, "f64": 8, "bf16": 4}[cfg["dt"]]  # the reply's element size (c5: fp32 G)
+        rows = cfg["rows"]
+        scale = 1 / np.sqrt(cols) if cfg["dt"] == "f64" else float(np.float32(1 / np.sqrt(cols)))
+
+        def shard(w):
+            A = torch.empty(rows[w - 1], cols, dtype=tdt, device="cuda")
+            b = torch.empty((rows[w - 1], k) if k > 1 else rows[w - 1], dtype=tdt, device="cuda")
+            M.generate(A, 61 + w, 0, 0, scale)
+            M.generate(b, 61 + w, 1, 0, 1.0)
+            return A, b
+
+        name = [f"/mpa_k{os.getpid()}_{uuid.uuid4().hex[:8]}"] if rank == 0 else [None]
+        if rank == 0:
+            comm = M.DistComm(n, placement, 0, name[0], cols * k * es, transport="hip")
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            comm = M.DistComm(n, placement, rank, name[0], cols * k * es, transport="hip")
+        keep = []
+        for w in (v for v in range(1, n + 1) if placement[v - 1] == rank):
+            keep.append(shard(w))
+            if k > 1:
+                comm.set_task_lsq_batch(w, *keep[-1])
+            else:
+                comm.set_task_lsq(w, *keep[-1])
+            if rank != 0:
+                rng = np.random.default_rng([17, w])
+                comm.set_delays(w, rng.exponential(cfg["delay_ms"] * 1e6, size=512).astype(np.int64))
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank != 0:
+            comm.serve()
+            dist.barrier()
+            comm.close()
+            dist.destroy_process_group()
+            return
+        names = ("held", "held_joined", "stale_deferred", "head_steps", "epoch_kernels", "task_launches")
+        c0 = {key: comm.counter(key) for key in names}
+        nwait = M.first_plus(5) if cfg["nwait"] == "first_plus5" else cfg["nwait"]
+        pool = M.MPIAsyncPool(n, epoch0=epoch0)
+        if k > 1:
+            x = torch.zeros(cols * k, device="cuda")
+            xb = torch.zeros(cols * k, dtype=torch.bfloat16, device="cuda")
+            isend = torch.zeros(n * cols * k, dtype=torch.bfloat16, device="cuda")
+            recv = torch.zeros(n * cols * k, device="cuda")
+        else:
+            x = torch.zeros(cols, dtype=tdt, device="cuda")
+            isend = torch.zeros(n * cols, dtype=tdt, device="cuda")
+            recv = torch.zeros(n * cols, dtype=tdt, device="cuda")
+        irecv = torch.zeros_like(recv)
+        epochs = cfg["epochs"]
+        # the native loop's per-epoch trace goes to fd 2 (C stdio): into a file for the replay
+        os.environ["MPA_DESCENT_TRACE"] = "1"
+        with tempfile.TemporaryFile(mode="w+") as tf:
+            saved = os.dup(2)
+            os.dup2(tf.fileno(), 2)
+            try:
+                if k > 1:
+                    M.lsqb_descent(pool, comm, x, xb, recv, isend, irecv, nwait, cfg["eta"], epochs,
+                                   stale_weight=cfg["stale"])
+                else:
+                    M.lsq_descent(pool, comm, x, recv, isend, irecv, nwait, cfg["eta"], epochs,
+                                  stale_weight=cfg["stale"])
+                torch.cuda.synchronize()
+            finally:
+                os.dup2(saved, 2)
+                os.close(saved)
+            tf.seek(0)
+            err = tf.read()
+        os.environ.pop("MPA_DESCENT_TRACE")
+        got = {key: comm.counter(key) - v for key, v in c0.items()}
+        x_end = x.clone()
+        M.waitall_(pool, recv, irecv)
+        torch.cuda.synchronize()
+        final_rep = [int(v) for v in pool.repochs]
+        final_chunks = recv.clone()
+        paths = [comm.payload_path(v) for v in range(1, n + 1) if placement[v - 1] != 0]
+        comm.shutdown()
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        errors = []
+        if paths != ["device"] * len(paths):
+            errors.append(("payload path", paths))
+        trace = [(int(m.group(1)), list(map(int, m.group(2).split())))
+                 for m in re.finditer(r"\[mpa descent\] epoch (\d+) repochs ([\d ]+) \|", err)]
+        if [e for e, _ in trace] != list(range(epoch0 + 1, epoch0 + epochs + 1)):
+            errors.append(("trace epochs", [e for e, _ in trace][:5], len(trace), err[-400:]))
+            result_q.put(("ok", errors))
+            return
+        # the fp64 replay on the device, each worker's gradient memoised per sent epoch
+        A64, b64 = [], []
+        for v in range(1, n + 1):
+            Av, bv = shard(v)
+            A64.append(Av.double())
+            b64.append(bv.double())
+            del Av, bv
+        memo = {}
+
+        def msg(xv):  # what the workers receive: the iterate (c5: its bf16 rounding, cols x 64)
+            return xv.to(torch.bfloat16).double().view(cols, k) if k > 1 else xv
+
+        def grad(i, e):
+            if (i, e) not in memo:
+                X = msg(xs[e - epoch0 - 1])
+                memo[(i, e)] = (A64[i].T @ (A64[i] @ X - b64[i])).reshape(-1)
+            return memo[(i, e)]
+
+        xs = [torch.zeros(cols * k, dtype=torch.float64, device="cuda")]  # xs[e-epoch0-1]: sent at epoch e
+        received = [False] * n
+        stale_remote = stale_local = 0
+        prev = [epoch0] * n
+        for e, rep in trace:
+            fresh = [i for i in range(n) if rep[i] == e]
+            for i in range(n):
+                received[i] = received[i] or rep[i] != epoch0
+                if rep[i] != prev[i] and rep[i] != e:  # a reply of an earlier epoch harvested in this call
+                    if placement[i] == 0:
+                        stale_local += 1
+                    else:
+                        stale_remote += 1
+            prev = rep
+            if cfg["nwait"] == "first_plus5":
+                ok = rep[0] == e and len(fresh) >= 6
+            else:
+                ok = len(fresh) >= cfg["nwait"]
+            if not ok:
+                errors.append(("nwait not satisfied", e, rep))
+            wts = [1.0 if rep[i] == e else (cfg["stale"] if received[i] else 0.0) for i in range(n)]
+            s = n / sum(wts) if sum(wts) > 0 else 0.0
+            upd = torch.zeros_like(xs[0])
+            for i in range(n):
+                if wts[i] != 0.0:
+                    upd += (wts[i] * s) * grad(i, rep[i])
+            xs.append(xs[-1] - cfg["eta"] * upd)
+        tol = cfg["tol"]
+        rel = float(torch.linalg.norm(x_end.double() - xs[-1]) / torch.linalg.norm(xs[-1]))
+        if not rel <= tol:
+            errors.append(("final iterate vs fp64 replay", rel))
+        ch = final_chunks.view(n, -1).double()
+        for i in range(n):
+            r = final_rep[i]
+            if r == epoch0:
+                continue
+            g = grad(i, r)
+            e_i = float(torch.linalg.norm(ch[i] - g) / torch.linalg.norm(g))
+            if not e_i <= tol:
+                errors.append(("final chunk", i, r, e_i))
+        if not stale_remote >= 1:
+            errors.append(("no remote stale harvest", stale_remote))
+        if config in ("c3", "c5") and not stale_local >= 1:
+            errors.append(("no stale harvest of the slow local worker", stale_local))
+        if config == "c3" and got["held"] != 0:
+            errors.append(("held a re-dispatch with nothing else of rank 0's in flight", got))
+        if config == "c5" and not (got["held"] >= 1 and got["held_joined"] >= 1):
+            errors.append(("no held re-dispatch joined a launch", got))
+        print("descent k-of-n %s epoch0 %d: %s, stale harvests local %d remote %d, iterate rel %.2e"
+              % (config, epoch0, got, stale_local, stale_remote, rel), flush=True)
+        result_q.put(("ok", errors))
+    except Exception:
+        result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
+        raise
+
+
 def armed_timeout_dist(rank, world, port, result_q):
     """A device-armed task whose doorbell never comes: rank 1 serves one least-squares
     worker, armed behind a one-wave doorbell wait bounded at MPA_WAIT_TIMEOUT_S = 2 s; rank 0 posts

@@ -134,6 +134,24 @@ def test_sched_eight_processes(built, config, epoch0):
     _run(dist_worker.lsq_sched_dist, 8, list(range(8)), config, epoch0, timeout=240)
 
 
+@pytest.mark.parametrize("config,epoch0", [("c3", 0), ("c4", 0), ("c4", 1000), ("c5", 0)])
+def test_native_kofn_descent_eight_processes(built, config, epoch0):
+    """The native k-of-n coordinator loop across processes -- bench.py's rank 0 at N > 1 for
+    c3 (fp32, nwait 6 of 8), c4 (fp64, first_plus(5), stale weight 0.5, epoch0 0 and 1000) and
+    c5 (bf16 batched, nwait 7) -- in the node's placement on GPU 0, ungated: the final iterate
+    equals a torch fp64 replay of the per-epoch repochs it traced, every final chunk the gradient
+    of the iterate sent at its repochs, remote and local stale harvests seen, a stale local
+    re-dispatch launched at once on rank 0 of the node's placement and held into the next launch
+    where rank 0 serves a second worker (c5)
+    (dist_worker.descent_kofn_dist; one process: tests/test_gpu.py
+    test_native_k_of_n_prearmed_with_stragglers)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    world = max(dist_worker.KOFN_CONFIGS[config]["placement"]) + 1
+    _run(dist_worker.descent_kofn_dist, world, config, epoch0, timeout=240)
+
+
 def test_armed_wait_timeout_cancels_the_task(built):
     """a device-armed task whose doorbell wait times out is cancelled (the one-wave
     door_wait_kernel stores the task's seq into its go word): no reply, no `done`, the error
