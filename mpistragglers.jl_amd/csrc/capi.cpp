@@ -294,6 +294,7 @@ int mpa_comm_set_delays(mpa_comm* comm, int64_t rank, const int64_t* delays_ns, 
     for (int64_t k = 0; k < count; ++k)
       if (delays_ns[k] < 0) mpa::fail(MPA_ARGUMENT_ERROR, "delays must be non-negative");
     c.task(rank).delays_ns.assign(delays_ns, delays_ns + count);
+    c.on_delays_changed(rank);
   });
 }
 

@@ -97,6 +97,7 @@ class Comm {
     return tasks_[size_t(rank - 1)];
   }
   virtual void on_task_changed(int64_t rank) { (void)rank; }
+  virtual void on_delays_changed(int64_t rank) { (void)rank; }
   virtual int64_t tasks_done(int64_t rank) = 0;
   virtual void shutdown() = 0;
   bool is_shutdown() const { return shutdown_; }

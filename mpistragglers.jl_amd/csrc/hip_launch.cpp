@@ -275,10 +275,16 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
       continue;
     }
     // The message is delivered now (stream-ordered after the exchange / stage-in); a
-    // delayed worker "sleeps" and only then computes: on the host timer thread, which
-    // launches the task when it is due (default), or on the device, a sleep kernel queued
-    // ahead of the task on the worker's stream (MPA_DELAY=device).
+    // delayed worker "sleeps" and only then computes: on the device, a deadline_kernel queued
+    // ahead of the task on the worker's stream until the post time + the delay (device_delay_ok:
+    // where no caller work on the NULL stream can wait behind it), or on the host timer thread,
+    // which launches the task when it is due.
     hipStream_t s = worker_stream(w);
+    const int64_t post_ns = int64_t(mono_ns());
+    const bool on_device = delay > 0 && device_delay_ok(s);
+    const int64_t sleep_ns = delay - (on_device ? deadline_lead_ns_ : delay_lead_ns_);
+    // (the clock map's refresh, if due, probes this stream while it is still idle)
+    const unsigned long long deadline = on_device && sleep_ns > 0 ? device_deadline(post_ns + sleep_ns, s) : 0;
     if (staged) stage_in({rank}, s);
     else after_exchange(s);
     std::function<void()> go;
@@ -310,25 +316,80 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
       };
     }
     if (int64_t* e = trace_entry(w)) e[kTDue] = e[kTPost] + delay;
-    // The oracle's worker replies exactly `delay` after its post; a launched task takes
-    // ~30-40 us more (launch, the kernel, the completion word crossing the bus).  That
-    // overhead is taken out of the sleep (delay_lead_ns_), or it would accumulate along every
-    // worker's chain of tasks: the gated kmap2_n9 replay drifted 1.2-1.9 ms from the
-    // oracle's latencies by its 100th call with 40 us per task (profiles/r04_gated_stall.txt).
-    const int64_t sleep_ns = delay - delay_lead_ns_;
-    // a device sleep holds the worker's stream: on a stream another worker shares (past the
-    // queue cap) it would delay that worker too, so those sleeps stay on the host timer
-    if (sleep_ns > 0 && delay_on_device_ && !stream_shared(s)) {
-      HIPCHECK(launch_sleep((unsigned long long)(double(sleep_ns) * rt_hz_ / 1e9), s));
+    // The oracle's worker replies exactly `delay` after its post; a task launched by the timer
+    // takes ~30-40 us more (launch, the kernel, the completion word crossing the bus), one
+    // queued behind a deadline ~8 us (its dispatch, the kernel, the word).  That overhead is
+    // taken out of the sleep, or it would accumulate along every worker's chain of tasks: the
+    // gated kmap2_n9 replay drifted 1.2-1.9 ms from the oracle's latencies by its 100th call
+    // with 40 us per task (profiles/r04_gated_stall.txt).
+    if (deadline) {
+      HIPCHECK(launch_deadline(deadline, spin_ticks(), err_dev_, s));
       n_sleeps_ += 1;
       go();
     } else if (sleep_ns > 0) {
-      defer(mono_ns() + uint64_t(sleep_ns), std::move(go));
+      defer(uint64_t(post_ns + sleep_ns), std::move(go));
     } else {
       go();
     }
   }
   emit();
+}
+
+// Device deadlines only where nothing can wait behind the sleeping wave but the worker's own
+// task: a stream of its own (past the queue cap workers share one), and no caller work on the
+// legacy NULL stream (HIP orders every NULL-stream command after all work queued on blocking
+// streams, profiles/r04_delay_on_device.txt): a worker process (serve() runs no caller code),
+// the native descent loop (its epochs are native code on the coordinator's own stream), or a
+// caller on a stream of its own.  MPA_DELAY=timer / =device force either.
+bool HipComm::device_delay_ok(hipStream_t s) const {
+  if (delay_mode_ == 1 || stream_shared(s)) return false;
+  if (delay_mode_ == 2) return true;
+  return role_ == SERVER || defer_end_ || !caller_null_;
+}
+
+// host steady-clock ns -> device s_memrealtime ticks: the latest sample, and the rate measured
+// between the first and the latest once they are a second apart (the two crystals drift by tens
+// of ppm: tens of us per second); refreshed every 250 ms by one probe on the worker's stream,
+// which is idle here (its previous task completed before the pool could re-post the worker)
+unsigned long long HipComm::device_deadline(int64_t host_ns, hipStream_t s) {
+  const int64_t now = int64_t(mono_ns());
+  if (!ck_n0_ || now - ck_n1_ > int64_t(kClockRecalNs)) {
+    int64_t t = 0, n = 0;
+    const int64_t rtt = clock_sample(s, &t, &n);
+    if (rtt >= 0 && rtt <= kClockMaxRttNs) {
+      if (!ck_n0_) {
+        ck_t0_ = t;
+        ck_n0_ = n;
+      }
+      ck_t1_ = t;
+      ck_n1_ = n;
+      ++n_clock_samples_;
+    } else if (!ck_n0_) {
+      fail(MPA_DEVICE_ERROR, "clock calibration: no probe round trip under %lld us", (long long)(kClockMaxRttNs / 1000));
+    }
+  }
+  const double rate = ck_n1_ - ck_n0_ >= kClockRateSpanNs ? double(ck_t1_ - ck_t0_) / double(ck_n1_ - ck_n0_) : rt_hz_ / 1e9;
+  const double d = double(ck_t1_) + double(host_ns - ck_n1_) * rate;
+  return d > 0 ? (unsigned long long)(d) : 0ull;
+}
+
+int64_t HipComm::clock_sample(hipStream_t s, int64_t* ticks, int64_t* ns) {
+  if (!clock_probe_)
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&clock_probe_), 64, hipHostMallocCoherent | hipHostMallocMapped));
+  __atomic_store_n(clock_probe_, 0ull, __ATOMIC_SEQ_CST);
+  const int64_t t0 = int64_t(mono_ns());
+  HIPCHECK(launch_clock_probe(reinterpret_cast<unsigned long long*>(clock_probe_), s));
+  for (uint64_t spins = 0; __atomic_load_n(clock_probe_, __ATOMIC_ACQUIRE) == 0; ++spins) {
+    if ((spins & 0xFFFF) == 0xFFFF && int64_t(mono_ns()) - t0 > 100000000) {  // 100 ms: a busy stream
+      HIPCHECK(hipStreamSynchronize(s));
+      return -1;
+    }
+    __builtin_ia32_pause();
+  }
+  const int64_t t1 = int64_t(mono_ns());
+  *ticks = int64_t(__atomic_load_n(clock_probe_, __ATOMIC_ACQUIRE));
+  *ns = t0 + (t1 - t0) / 2;
+  return t1 - t0;
 }
 
 void HipComm::defer(uint64_t due, std::function<void()> go) {
@@ -365,10 +426,15 @@ void HipComm::timer_loop() {
       // spin with the lock released; a task deferred meanwhile with an earlier deadline moves
       // tfront_ below `due` and ends the spin (the loop then takes the new front), as does a stop
       lk.unlock();
-      // yielding: on a core it shares with the coordinator's wait, neither holds the other off
-      while (mono_ns() < due && tfront_.load(std::memory_order_acquire) >= due &&
-             !tstop_spin_.load(std::memory_order_acquire))
-        std::this_thread::yield();
+      // yielding until the last 50 us (on a core it shares with the coordinator's wait neither
+      // holds the other off), then pause-spinning: a yield that gives the core away for a
+      // scheduler slice right at the deadline made the launch late
+      uint64_t t;
+      while ((t = mono_ns()) < due && tfront_.load(std::memory_order_acquire) >= due &&
+             !tstop_spin_.load(std::memory_order_acquire)) {
+        if (t + kTimerPauseNs < due) std::this_thread::yield();
+        else __builtin_ia32_pause();
+      }
       lk.lock();
       continue;
     }

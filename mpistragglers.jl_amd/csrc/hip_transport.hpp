@@ -61,6 +61,17 @@ constexpr uint64_t kTimerSpinNs = 1000000;
 // A delayed task's own overhead (launch -> completion word seen, ~30-40 us: the median latency
 // deviation of the gated replays, profiles/r04_gated_stall.txt) comes out of its sleep.
 constexpr int64_t kDelayLeadNs = 35000;  // the straggler timer spins the last 1 ms before a due launch
+constexpr uint64_t kTimerPauseNs = 50000;  // ... yielding the core until the last 50 us, then pause-spinning
+// A device-deadline delay (deadline_kernel already queued ahead of the task): what remains after
+// the deadline is the task's dispatch behind it, the task itself and its completion word
+// crossing the bus (MPA_DEADLINE_LEAD_NS overrides it)
+constexpr int64_t kDeadlineLeadNs = 8000;
+// the host <-> device clock map behind device deadlines is refreshed at most this often (one
+// probe round trip on the delayed worker's idle stream), a sample with a longer round trip is
+// dropped, and the rate is measured over at least kClockRateSpanNs
+constexpr uint64_t kClockRecalNs = 250000000;
+constexpr int64_t kClockMaxRttNs = 40000;
+constexpr int64_t kClockRateSpanNs = 1000000000;
 // batched multi-iterate task: pass-1 / pass-2 workgroups per launch (= resident: 1 x 512 /
 // 2 x 256 threads per CU by VGPRs), and the most row ranges a pass-2 task is split into
 constexpr int kLsqbGrid1 = 512;  // two 8-wave workgroups per CU: pass 1 4.74-4.88 -> 5.11 TB/s (profiles/r01_lsqb_grid.txt)
@@ -247,7 +258,10 @@ class HipComm final : public Comm {
   // epoch step, up to 5.7 ms per harvest; profiles/r05_null_stream.txt).  The comm's stream is
   // a blocking stream itself, so HIP still orders it with the caller's NULL-stream work both
   // ways.  MPA_OWN_COORD=0 keeps the NULL stream.
-  void set_stream(hipStream_t s) { coord_ = (s == nullptr || s == hipStreamLegacy) && own_coord_ ? own_coord_ : s; }
+  void set_stream(hipStream_t s) {
+    caller_null_ = s == nullptr || s == hipStreamLegacy;
+    coord_ = caller_null_ && own_coord_ ? own_coord_ : s;
+  }
   hipStream_t stream() const { return coord_; }
 
   void begin_call(const CallBufs& b) override {
@@ -361,6 +375,7 @@ class HipComm final : public Comm {
   void shutdown() override;
 
   void on_task_changed(int64_t rank) override;
+  void on_delays_changed(int64_t rank) override;
 
   // ---- worker process: watch the doorbells of the workers served here ----
   // Least-squares workers without a delay schedule whose messages arrive in this GPU's slot
@@ -920,9 +935,25 @@ class HipComm final : public Comm {
   std::mutex tfail_mu_;
   std::string tfail_msg_;
   std::atomic<int64_t> n_timer_late_{0};  // deferred launches issued > 1 ms after due (counter 'timer_late')
-  bool delay_on_device_ = false;          // MPA_DELAY=device: sleep kernels instead of the timer
-  int64_t delay_lead_ns_ = kDelayLeadNs;  // MPA_DELAY_LEAD_NS: a delayed task's launch overhead, out of its sleep
-  int64_t n_sleeps_ = 0;
+  // Injected delays (launch_tasks): MPA_DELAY=timer the host timer always, =device a device
+  // deadline wherever the worker's stream is its own, unset (auto) a device deadline where no
+  // caller work on the legacy NULL stream can meet it (a CU-masked worker stream is a blocking
+  // stream: every NULL-stream command would wait for the sleeping straggler, round 4's
+  // objection): in a worker process, inside the native descent loop, or for a caller on a stream
+  // of its own; the host timer otherwise
+  int delay_mode_ = 0;                     // 0 auto, 1 timer, 2 device
+  bool caller_null_ = true;                // the caller's stream (set_stream) is the NULL stream
+  int64_t delay_lead_ns_ = kDelayLeadNs;   // MPA_DELAY_LEAD_NS: the timer's launch overhead, out of its sleep
+  int64_t deadline_lead_ns_ = kDeadlineLeadNs;
+  // host <-> device clock map (steady-clock ns, s_memrealtime ticks): the first sample and the latest
+  int64_t ck_t0_ = 0, ck_n0_ = 0, ck_t1_ = 0, ck_n1_ = 0;
+  int64_t n_clock_samples_ = 0;
+  bool device_delay_ok(hipStream_t s) const;
+  unsigned long long device_deadline(int64_t host_ns, hipStream_t s);
+  // one probe round trip on `s` (idle): (device ticks, host ns) at its midpoint, returns the round
+  // trip in ns (or -1: the probe had not landed after 100 ms)
+  int64_t clock_sample(hipStream_t s, int64_t* ticks, int64_t* ns);
+  int64_t n_sleeps_ = 0;  // delayed tasks queued behind a device deadline
   int64_t n_armed_ = 0;   // server: tasks launched device-armed (counter 'armed')  // delayed tasks (a sleep kernel before the task, counter 'sleeps')
 
  public:

@@ -309,14 +309,27 @@ hipError_t launch_door_wait(const unsigned long long* door, unsigned long long s
 // sleep(rand()) between its Irecv and its reply (examples/iterative_example.jl:74,
 // test/kmap2.jl:95).  No host thread sits between the schedule and the latency the pool
 // records; one wave holds no CU anyone else needs.
-__global__ void __launch_bounds__(64) sleep_kernel(unsigned long long ticks) {
+// An injected straggler delay on the device: one wave waits on its worker's stream, ahead of
+// the task, until an ABSOLUTE deadline on the GPU's constant 100 MHz clock (the host's post time
+// + the delay, mapped through the clock calibration, HipComm::device_deadline): when the stream
+// reaches it does not matter, and no host thread has to wake up on time.  Bounded (err bit 256).
+__global__ void __launch_bounds__(64) deadline_kernel(unsigned long long deadline, unsigned long long bound,
+                                                       unsigned* err) {
   if (threadIdx.x) return;
   const unsigned long long t0 = rt_now();
-  while (rt_now() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  for (;;) {
+    const unsigned long long t = rt_now();
+    if (t >= deadline) break;
+    if (t - t0 > bound) {
+      __hip_atomic_fetch_or(err, 256u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
 }
 
-hipError_t launch_sleep(unsigned long long ticks, hipStream_t s) {
-  hipLaunchKernelGGL(sleep_kernel, dim3(1), dim3(64), 0, s, ticks);
+hipError_t launch_deadline(unsigned long long deadline, unsigned long long bound, unsigned* err, hipStream_t s) {
+  hipLaunchKernelGGL(deadline_kernel, dim3(1), dim3(64), 0, s, deadline, bound, err);
   return hipGetLastError();
 }
 

@@ -395,8 +395,9 @@ hipError_t launch_kmap(const KmapArgs& a, hipStream_t s);
 // the task cancels itself, and sets err bit 64), then acquires at system scope; the task runs behind it
 hipError_t launch_door_wait(const unsigned long long* door, unsigned long long seq, unsigned long long spin_ticks,
                             unsigned* err, unsigned long long* cancel, hipStream_t s);
-// one wave that spins `ticks` of s_memrealtime (a delayed worker's sleep, on its stream)
-hipError_t launch_sleep(unsigned long long ticks, hipStream_t s);
+// one wave that waits until s_memrealtime reaches `deadline` (a delayed worker's sleep, ahead of
+// its task on its stream), at most `bound` ticks (then err bit 256)
+hipError_t launch_deadline(unsigned long long deadline, unsigned long long bound, unsigned* err, hipStream_t s);
 // a worker process moves its device doorbell word (a device-armed task's cancel / restore,
 // hip_server.cpp disarm_all): *door = desired if it holds expect; the value it held goes to
 // *old_out (host-pinned)

@@ -64,13 +64,14 @@ struct Tile {
   using P = Pack<T>;
   static constexpr int E = P::E;
   P d[RB][VPL];
-  // the fp64 fused-head variant's b values, loaded with the tile (load_b): under the head's
-  // control flow each row's b load was issued in its own branch and waited for there, one memory
-  // round trip per row (c1's 16-row tiles: most of its tasks' time); clamped, they issue together,
-  // before the token wait for a prefetched tile.  fp32 keeps the per-row loads: there the moved
-  // loads changed how the compiler contracted the row's update, and the head variant no longer
-  // matched the plain one bit for bit (r05bf)
-  static constexpr bool kHeadB = (MODE & M_HEAD) != 0 && sizeof(T) == 8;
+  // the fused-head variants' b values, loaded with the tile (load_b): under the head's control
+  // flow each row's b load was issued in its own branch and waited for there, one memory round
+  // trip per row (c1's 16-row tiles: most of its tasks' time); clamped, they issue together,
+  // before the token wait for a prefetched tile.  (fp32 kept its per-row loads in round 5: moving
+  // them changed how the compiler contracted the row's update, r05bf; compute() now spells its
+  // fused multiply-adds out, so the variants round alike whatever the loads' placement.)  Every
+  // load() of a head tile is followed by its load_b(), the prefetching loop's included.
+  static constexpr bool kHeadB = (MODE & M_HEAD) != 0;
   [[maybe_unused]] T bq[kHeadB ? RB : 1];
 
   // rows [base, base+RB): out-of-range rows/vectors either branch (default) or read a
@@ -111,6 +112,15 @@ struct Tile {
     }
   }
 
+  // The row's dot and the g update are written as explicit fused multiply-adds in a fixed
+  // order, so that every kernel variant (plain, head, armed, tail, pre-armed) rounds them the
+  // same way whatever the surrounding code lets the compiler contract (moving
+  // the fp32 head variant's b loads once changed its contraction by 1 ulp).
+  static __device__ __forceinline__ T fmac(T a, T b, T c) {
+    if constexpr (sizeof(T) == 8) return __builtin_fma(a, b, c);
+    else return __builtin_fmaf(a, b, c);
+  }
+
   __device__ __forceinline__ void compute(const T* __restrict__ bv, int64_t base, int64_t rows, const P (&xr)[VPL],
                                           P (&g)[VPL]) const {
     T dot[RB];
@@ -120,7 +130,7 @@ struct Tile {
 #pragma unroll
       for (int v = 0; v < VPL; ++v)
 #pragma unroll
-        for (int e = 0; e < E; ++e) s += d[rb][v].v[e] * xr[v].v[e];
+        for (int e = 0; e < E; ++e) s = fmac(d[rb][v].v[e], xr[v].v[e], s);
       dot[rb] = s;
     }
 #pragma unroll
@@ -134,7 +144,7 @@ struct Tile {
 #pragma unroll
       for (int v = 0; v < VPL; ++v)
 #pragma unroll
-        for (int e = 0; e < E; ++e) g[v].v[e] += res * d[rb][v].v[e];
+        for (int e = 0; e < E; ++e) g[v].v[e] = fmac(res, d[rb][v].v[e], g[v].v[e]);
     }
   }
 };
@@ -331,15 +341,24 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
 
   if constexpr (MODE & M_PREFETCH) {
     Tile<T, VPL, RB, MODE> t1;
-    if (base < hi && !pre) t0.load(A, base, rows, a.lda, lane, vok);
+    if (base < hi && !pre) {
+      t0.load(A, base, rows, a.lda, lane, vok);
+      t0.load_b(bv, base, rows);
+    }
     for (;;) {
       const int64_t b1 = base + step;
       if (base >= hi) break;
-      if (b1 < hi) t1.load(A, b1, rows, a.lda, lane, vok);
+      if (b1 < hi) {
+        t1.load(A, b1, rows, a.lda, lane, vok);
+        t1.load_b(bv, b1, rows);
+      }
       t0.compute(bv, base, rows, xr, g);
       const int64_t b2 = b1 + step;
       if (b1 >= hi) break;
-      if (b2 < hi) t0.load(A, b2, rows, a.lda, lane, vok);
+      if (b2 < hi) {
+        t0.load(A, b2, rows, a.lda, lane, vok);
+        t0.load_b(bv, b2, rows);
+      }
       t1.compute(bv, b1, rows, xr, g);
       base = b2;
     }

@@ -126,9 +126,11 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   // injected straggler delays: the host timer (default) or a sleep kernel ahead of the task on
   // an unshared worker stream (MPA_DELAY=device); the launch overhead taken out of each sleep
   const char* dl = std::getenv("MPA_DELAY");
-  delay_on_device_ = dl && !std::strcmp(dl, "device");
+  delay_mode_ = dl && !std::strcmp(dl, "timer") ? 1 : dl && !std::strcmp(dl, "device") ? 2 : 0;
   const char* lead = std::getenv("MPA_DELAY_LEAD_NS");
   if (lead) delay_lead_ns_ = std::atoll(lead);
+  const char* dlead = std::getenv("MPA_DEADLINE_LEAD_NS");
+  if (dlead) deadline_lead_ns_ = std::atoll(dlead);
   // how an armed task waits: one wave ahead of it (default) or every workgroup in-kernel
   const char* aw = std::getenv("MPA_ARM_WAIT");
   arm_wave_ = !(aw && !std::strcmp(aw, "kernel"));
@@ -519,6 +521,28 @@ void HipComm::on_task_changed(int64_t rank) {
   if (ts.kind == MPA_TASK_LSQ_BATCH) prepare_lsqb(rank, ts);
 }
 
+// A delay schedule registered for a worker of this process: its stream now (a stream is never
+// created inside a timed schedule), and the first host <-> device clock sample behind device
+// deadlines (best of 16 round trips on that idle stream).
+void HipComm::on_delays_changed(int64_t rank) {
+  HipWorker& w = w_[size_t(rank - 1)];
+  if (!w.here || tasks_[size_t(rank - 1)].delays_ns.empty()) return;
+  hipStream_t s = worker_stream(w);
+  if (ck_n0_) return;
+  int64_t best = INT64_MAX;
+  for (int k = 0; k < 16; ++k) {
+    int64_t t = 0, n = 0;
+    const int64_t rtt = clock_sample(s, &t, &n);
+    if (rtt >= 0 && rtt < best) {
+      best = rtt;
+      ck_t0_ = ck_t1_ = t;
+      ck_n0_ = ck_n1_ = n;
+    }
+  }
+  if (best == INT64_MAX) fail(MPA_DEVICE_ERROR, "clock calibration: no probe landed");
+  n_clock_samples_ = 1;
+}
+
 void HipComm::launch_local(const std::vector<int64_t>& posted) {
   std::vector<int64_t> here;
   for (int64_t rank : posted) {
@@ -817,7 +841,8 @@ int64_t HipComm::counter(const char* name) const {
   if (k == "prearm_cancelled") return n_pre_cancel_;
   if (k == "prearm_same") return n_pre_same_;  // released with the step's predicted arguments
   if (k == "armed") return n_armed_;  // server: tasks launched device-armed (some may be cancelled)
-  if (k == "sleeps") return n_sleeps_;  // delayed tasks: a sleep kernel ran before the task
+  if (k == "sleeps") return n_sleeps_;  // delayed tasks queued behind a device deadline (deadline_kernel)
+  if (k == "clock_samples") return n_clock_samples_;  // host <-> device clock samples behind the deadlines
   if (k == "timer_late") return n_timer_late_.load(std::memory_order_relaxed);  // > 1 ms late timer launches
   if (k == "queues") return queue_streams(dev_);  // CU-masked streams (HSA queues) the process holds
   if (k == "shared_worker_streams") {  // workers whose stream another worker or comm also uses

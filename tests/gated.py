@@ -172,20 +172,26 @@ def kmap2_replay(M, sc, delays, own_stream=False):
 
 TRACE_CAP = 1 << 14
 F = {k: j for j, k in enumerate(("rank", "seq", "post", "due", "call", "ret", "start", "pub", "gate", "seen", "harvest"))}
-LEAD_NS = 35_000  # the transport's default MPA_DELAY_LEAD_NS
+LEAD_NS = 35_000  # the transport's default MPA_DELAY_LEAD_NS (host timer)
+DEADLINE_LEAD_NS = 8_000  # ... MPA_DEADLINE_LEAD_NS (a task queued behind a device deadline)
 
 
 def task_parts(e):
     """(ms) where a task's time went against the oracle's clock: timer (the launch call against
-    its due time less the launch lead), launch (the call itself), queue (call returned ->
-    kernel started), kernel, visible (completion store, or the gate step's start if that came
-    later -> the gate saw it: the coordinator's own lateness), harvest (seen -> taken); `late` =
-    completion store - due (the task's own lateness)."""
+    its due time less the launch lead; a task queued behind a device deadline at its post has
+    none: its `deadline` part is the kernel's start against its due time less that lead), launch
+    (the call itself), queue (call returned -> kernel started), kernel, visible (completion store,
+    or the gate step's start if that came later -> the gate saw it: the coordinator's own
+    lateness), harvest (seen -> taken); `late` = completion store - due (the task's own
+    lateness)."""
     ms = lambda a, b: round((e[F[a]] - e[F[b]]) / 1e6, 3) if e[F[a]] and e[F[b]] else None
     due = e[F["due"]]
     delayed = due - e[F["post"]] > LEAD_NS
+    # launched at its post, long before its due time: it waited behind a deadline_kernel
+    on_device = delayed and e[F["call"]] and e[F["call"]] < due - LEAD_NS - 500_000
     p = {"task": "r%d#%d" % (e[F["rank"]], e[F["seq"]]),
-         "timer": round((e[F["call"]] - (due - LEAD_NS)) / 1e6, 3) if delayed and e[F["call"]] else None,
+         "timer": round((e[F["call"]] - (due - LEAD_NS)) / 1e6, 3) if delayed and e[F["call"]] and not on_device else None,
+         "deadline": round((e[F["start"]] - (due - DEADLINE_LEAD_NS)) / 1e6, 3) if on_device and e[F["start"]] else None,
          "launch": ms("ret", "call"), "queue": ms("start", "ret"), "kernel": ms("pub", "start"),
          "visible": (round((e[F["seen"]] - max(e[F["pub"]], e[F["gate"]])) / 1e6, 3)
                      if e[F["seen"]] and e[F["pub"]] else None),
@@ -225,7 +231,7 @@ def hop_check(sc, got, trace, task_tol=1e-3, obs_tol=1e-3, lat_tol=50e-6):
     the op that harvested it is the call whose host-time window holds its harvest.
 
     Returns (misses, stats): misses are (kind, op, pool position, ms, tolerance ms); stats the
-    p50 / max of each hop in ms."""
+    p50 / p99 of |hop| / max of |hop| of each hop in ms."""
     mg = make_golden()
     _, sim = mg.run_scenario(sc, return_sim=True)
     events, done_at = {}, {}
@@ -273,7 +279,8 @@ def hop_check(sc, got, trace, task_tol=1e-3, obs_tol=1e-3, lat_tol=50e-6):
             bad.append(("harvest", k, i, round(obs_dev * 1e3, 3), obs_tol * 1e3))
     hops["between_calls"] = [(got[k]["t_ns"][0] - got[k - 1]["t_ns"][1] - sc["ops"][k].get("advance_ns", 0)) / 1e9
                              for k in range(1, len(got))]
-    stats = {key: (round(float(np.median(v)) * 1e3, 3), round(float(np.max(np.abs(v))) * 1e3, 3))
+    stats = {key: (round(float(np.median(v)) * 1e3, 3), round(float(np.percentile(np.abs(v), 99)) * 1e3, 3),
+                   round(float(np.max(np.abs(v))) * 1e3, 3))
              for key, v in hops.items() if v}
     return sorted(bad, key=lambda b: (b[1], b[2])), stats
 
@@ -299,7 +306,7 @@ def trace_stats(trace):
     """Percentiles (p50 / p99 / max, ms) of each part over every traced task."""
     parts = [task_parts(e) for e in trace]
     st = {}
-    for key in ("timer", "launch", "queue", "kernel", "visible", "harvest", "late"):
+    for key in ("timer", "deadline", "launch", "queue", "kernel", "visible", "harvest", "late"):
         v = np.asarray([p[key] for p in parts if p[key] is not None])
         if len(v):
             st[key] = (round(float(np.median(v)), 3), round(float(np.percentile(v, 99)), 3), round(float(v.max()), 3))
@@ -370,16 +377,21 @@ class HostWatchdog:
 
 
 def warm_kernels(M, torch, n):
-    """Load the task / sleep / exchange code objects before a timing-sensitive trace (a
-    first launch loads its code object)."""
-    comm = M.DeviceComm(n)
-    for r in range(1, n + 1):
-        comm.set_task(r, "kmap2")
-        comm.set_delays(r, [1000, 0])
-    pool = M.MPIAsyncPool(n)
-    s = torch.zeros(1, dtype=torch.float64, device="cuda")
-    rb = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
-    for _ in range(3):
-        M.asyncmap_(pool, s, rb, torch.zeros(n, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), comm, nwait=n)
-    torch.cuda.synchronize()
-    comm.close()
+    """Load the task / deadline / exchange code objects before a timing-sensitive trace (a
+    first launch loads its code object): delayed tasks by the host timer (the caller on the NULL
+    stream) and behind device deadlines (on a stream of its own)."""
+    for own in (False, True):
+        ctx = torch.cuda.stream(torch.cuda.Stream()) if own else contextlib.nullcontext()
+        with ctx:
+            comm = M.DeviceComm(n)
+            for r in range(1, n + 1):
+                comm.set_task(r, "kmap2")
+                comm.set_delays(r, [100_000, 0])
+            pool = M.MPIAsyncPool(n)
+            s = torch.zeros(1, dtype=torch.float64, device="cuda")
+            rb = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+            for _ in range(3):
+                M.asyncmap_(pool, s, rb, torch.zeros(n, dtype=torch.float64, device="cuda"), torch.zeros_like(rb), comm,
+                            nwait=n)
+            torch.cuda.synchronize()
+            comm.close()

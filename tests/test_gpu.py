@@ -187,11 +187,12 @@ def test_queue_cap(M, torch_mod):
 
 
 def test_device_delays_only_on_unshared_streams(M, torch_mod, monkeypatch):
-    """MPA_DELAY=device (opt-in): a delayed task sleeps in a one-wave kernel ahead
-    of it on its worker's stream -- but only where that stream is the worker's own: past the
-    queue cap workers share streams, and a sleep there would hold the other worker's tasks,
-    so those delays stay on the host timer.  16 workers over 9 streams: one sleep kernel per
-    unshared worker, every reply correct."""
+    """MPA_DELAY=device (forced; by default only where no caller work on the NULL stream can meet
+    it): a delayed task waits behind a one-wave deadline kernel ahead of it on its worker's
+    stream -- but only where that stream is the worker's own: past the queue cap workers share
+    streams, and a wait there would hold the other worker's tasks, so those delays stay on the
+    host timer.  16 workers over 9 streams: one deadline kernel per unshared worker, every reply
+    correct."""
     monkeypatch.setenv("MPA_DELAY", "device")
     torch = torch_mod
     c = M.DeviceComm(16)
@@ -210,8 +211,8 @@ def test_device_delays_only_on_unshared_streams(M, torch_mod, monkeypatch):
 
 
 def _straggler_hold(M, torch):
-    """Three nwait = 1 calls while worker 2's 400 ms delay sleeps ON THE DEVICE (a sleep kernel on
-    its worker stream): the wall time of each call."""
+    """Three nwait = 1 calls while worker 2's 400 ms delay sleeps ON THE DEVICE (a deadline kernel
+    on its worker stream): the wall time of each call."""
     import time
     c = M.DeviceComm(2)
     for r in (1, 2):
@@ -240,7 +241,7 @@ def test_running_straggler_does_not_hold_the_coordinator(M, torch_mod, monkeypat
     exchange that re-dispatched worker 1 waited for worker 2's running kernel (c3: 0.1-0.6 ms per
     epoch step, up to 5.7 ms per harvest; profiles/r05_null_stream.txt).  The comm coordinates on
     a stream of its own instead (hip_transport.hpp set_stream): calls 2 and 3 re-dispatch worker 1
-    in milliseconds while worker 2's 400 ms sleep kernel runs."""
+    in milliseconds while worker 2's 400 ms deadline kernel runs."""
     monkeypatch.setenv("MPA_DELAY", "device")
     torch = torch_mod
     t, sleeps, ok = _straggler_hold(M, torch)
@@ -251,8 +252,13 @@ def test_running_straggler_does_not_hold_the_coordinator(M, torch_mod, monkeypat
 
 
 @pytest.mark.timing
-def test_delay_calibration(M, torch_mod):
-    """An injected delay of d ms shows up as a latency of d ms (within 0.5 ms)."""
+@pytest.mark.parametrize("path", ["timer", "deadline"])
+def test_delay_calibration(M, torch_mod, path):
+    """An injected delay of d ms shows up as a latency of d ms (within 0.5 ms), by either path:
+    the host timer (the caller on torch's default stream, HIP's NULL stream: a device deadline
+    would hold every NULL-stream command) and a device deadline (the caller on a stream of its
+    own: deadline_kernel queued ahead of the task, no host thread involved; within 0.2 ms)."""
+    import contextlib
     torch = torch_mod
     _warm_kernels(M, torch, 2)
     comm = M.DeviceComm(2)
@@ -260,24 +266,33 @@ def test_delay_calibration(M, torch_mod):
         comm.set_task(r, "echo")
         comm.set_delays(r, [d])
     pool = M.MPIAsyncPool(2)
-    s = torch.zeros(2, device="cuda")
-    # three calls in a row within 0.5 ms; a run with a miss gets one rerun (a stall of the box
-    # inflates one call's latency, profiles/r04_gated_stall.txt)
-    for attempt in range(2):
-        if attempt:
-            __import__("time").sleep(10)  # a noisy spell of the box passes
-        lat = []
-        with gated_mod().no_gc():
-            for _ in range(3):
-                M.asyncmap_(pool, s, torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"),
-                            torch.zeros(4, device="cuda"), comm, nwait=2)
-                # the delay is dispatch -> reply (the task's ~35 us launch overhead is inside it)
-                lat.append((float(pool.latency[0]), float(pool.latency[1])))
-        ok = all(abs(a - 0.020) < 0.5e-3 and abs(b - 0.007) < 0.5e-3 for a, b in lat)
-        print("delay calibration run %d: %s" % (attempt, lat))
-        if ok:
-            break
+    tol = 0.5e-3 if path == "timer" else 0.2e-3
+    ctx = torch.cuda.stream(torch.cuda.Stream()) if path == "deadline" else contextlib.nullcontext()
+    with ctx:
+        s = torch.zeros(2, device="cuda")
+        # three calls in a row; a run with a miss gets one rerun (a stall of the box inflates one
+        # call's latency, profiles/r04_gated_stall.txt)
+        for attempt in range(2):
+            if attempt:
+                __import__("time").sleep(10)  # a noisy spell of the box passes
+            lat = []
+            with gated_mod().no_gc():
+                for _ in range(3):
+                    M.asyncmap_(pool, s, torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda"),
+                                torch.zeros(4, device="cuda"), comm, nwait=2)
+                    # the delay is dispatch -> reply (the task's launch overhead is inside it)
+                    lat.append((float(pool.latency[0]), float(pool.latency[1])))
+            ok = all(abs(a - 0.020) < tol and abs(b - 0.007) < tol for a, b in lat)
+            print("delay calibration (%s) run %d: %s" % (path, attempt, lat))
+            if ok:
+                break
+        torch.cuda.current_stream().synchronize()
     assert ok, lat
+    # which path ran: deadline kernels (and the clock samples behind them) or the timer
+    if path == "deadline":
+        assert comm.counter("sleeps") >= 6 and comm.counter("clock_samples") >= 1
+    else:
+        assert comm.counter("sleeps") == 0
 
 
 def _lsq_case(M, torch, dtype, rows, cols, lda=None, seed=3, nworkers=1, grid=None):
