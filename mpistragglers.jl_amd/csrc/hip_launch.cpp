@@ -283,8 +283,7 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
     const int64_t post_ns = int64_t(mono_ns());
     const bool on_device = delay > 0 && device_delay_ok(s);
     const int64_t sleep_ns = delay - (on_device ? deadline_lead_ns_ : delay_lead_ns_);
-    // (the clock map's refresh, if due, probes this stream while it is still idle)
-    const unsigned long long deadline = on_device && sleep_ns > 0 ? device_deadline(post_ns + sleep_ns, s) : 0;
+    const unsigned long long deadline = on_device && sleep_ns > 0 ? device_deadline(post_ns + sleep_ns) : 0;
     if (staged) stage_in({rank}, s);
     else after_exchange(s);
     std::function<void()> go;
@@ -349,37 +348,23 @@ bool HipComm::device_delay_ok(hipStream_t s) const {
 
 // host steady-clock ns -> device s_memrealtime ticks: the latest sample, and the rate measured
 // between the first and the latest once they are a second apart (the two crystals drift by tens
-// of ppm: tens of us per second); refreshed every 250 ms by one probe on the worker's stream,
-// which is idle here (its previous task completed before the pool could re-post the worker)
-unsigned long long HipComm::device_deadline(int64_t host_ns, hipStream_t s) {
-  const int64_t now = int64_t(mono_ns());
-  if (!ck_n0_ || now - ck_n1_ > int64_t(kClockRecalNs)) {
-    int64_t t = 0, n = 0;
-    const int64_t rtt = clock_sample(s, &t, &n);
-    if (rtt >= 0 && rtt <= kClockMaxRttNs) {
-      if (!ck_n0_) {
-        ck_t0_ = t;
-        ck_n0_ = n;
-      }
-      ck_t1_ = t;
-      ck_n1_ = n;
-      ++n_clock_samples_;
-    } else if (!ck_n0_) {
-      fail(MPA_DEVICE_ERROR, "clock calibration: no probe round trip under %lld us", (long long)(kClockMaxRttNs / 1000));
-    }
-  }
+// of ppm: tens of us per second).  The samples come from the first calibration
+// (on_delays_changed) and the sampling thread (clock_loop); nothing here touches the GPU.
+unsigned long long HipComm::device_deadline(int64_t host_ns) {
+  std::lock_guard<std::mutex> g(ck_mu_);
+  if (!ck_n0_) fail(MPA_ERROR, "device deadline without a clock calibration");
   const double rate = ck_n1_ - ck_n0_ >= kClockRateSpanNs ? double(ck_t1_ - ck_t0_) / double(ck_n1_ - ck_n0_) : rt_hz_ / 1e9;
   const double d = double(ck_t1_) + double(host_ns - ck_n1_) * rate;
   return d > 0 ? (unsigned long long)(d) : 0ull;
 }
 
 int64_t HipComm::clock_sample(hipStream_t s, int64_t* ticks, int64_t* ns) {
-  if (!clock_probe_)
-    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&clock_probe_), 64, hipHostMallocCoherent | hipHostMallocMapped));
-  __atomic_store_n(clock_probe_, 0ull, __ATOMIC_SEQ_CST);
+  if (!ck_probe_)
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&ck_probe_), 64, hipHostMallocCoherent | hipHostMallocMapped));
+  __atomic_store_n(ck_probe_, 0ull, __ATOMIC_SEQ_CST);
   const int64_t t0 = int64_t(mono_ns());
-  HIPCHECK(launch_clock_probe(reinterpret_cast<unsigned long long*>(clock_probe_), s));
-  for (uint64_t spins = 0; __atomic_load_n(clock_probe_, __ATOMIC_ACQUIRE) == 0; ++spins) {
+  HIPCHECK(launch_clock_probe(reinterpret_cast<unsigned long long*>(ck_probe_), s));
+  for (uint64_t spins = 0; __atomic_load_n(ck_probe_, __ATOMIC_ACQUIRE) == 0; ++spins) {
     if ((spins & 0xFFFF) == 0xFFFF && int64_t(mono_ns()) - t0 > 100000000) {  // 100 ms: a busy stream
       HIPCHECK(hipStreamSynchronize(s));
       return -1;
@@ -387,9 +372,42 @@ int64_t HipComm::clock_sample(hipStream_t s, int64_t* ticks, int64_t* ns) {
     __builtin_ia32_pause();
   }
   const int64_t t1 = int64_t(mono_ns());
-  *ticks = int64_t(__atomic_load_n(clock_probe_, __ATOMIC_ACQUIRE));
+  *ticks = int64_t(__atomic_load_n(ck_probe_, __ATOMIC_ACQUIRE));
   *ns = t0 + (t1 - t0) / 2;
   return t1 - t0;
+}
+
+// The sampling thread of the clock map: one probe every 250 ms on a stream of its own, kept
+// when its round trip is short (the midpoint is then within a few us of the probe's stamp).
+void HipComm::clock_loop() {
+  (void)hipSetDevice(dev_);
+  std::unique_lock<std::mutex> lk(tmu_ck_);
+  for (;;) {
+    if (ck_cv_.wait_for(lk, std::chrono::nanoseconds(kClockRecalNs), [this]() { return ck_stop_; })) break;
+    lk.unlock();
+    int64_t t = 0, n = 0, rtt = -1;
+    try {
+      rtt = clock_sample(ck_stream_, &t, &n);
+    } catch (...) {
+      rtt = -1;  // (the map keeps its last sample)
+    }
+    if (rtt >= 0 && rtt <= kClockMaxRttNs) {
+      std::lock_guard<std::mutex> g(ck_mu_);
+      ck_t1_ = t;
+      ck_n1_ = n;
+      n_clock_samples_.fetch_add(1, std::memory_order_relaxed);
+    }
+    lk.lock();
+  }
+}
+
+void HipComm::stop_clock() {
+  {
+    std::lock_guard<std::mutex> g(tmu_ck_);
+    ck_stop_ = true;
+  }
+  ck_cv_.notify_all();
+  if (ck_thread_.joinable()) ck_thread_.join();
 }
 
 void HipComm::defer(uint64_t due, std::function<void()> go) {

@@ -66,9 +66,10 @@ constexpr uint64_t kTimerPauseNs = 50000;  // ... yielding the core until the la
 // the deadline is the task's dispatch behind it, the task itself and its completion word
 // crossing the bus (MPA_DEADLINE_LEAD_NS overrides it)
 constexpr int64_t kDeadlineLeadNs = 8000;
-// the host <-> device clock map behind device deadlines is refreshed at most this often (one
-// probe round trip on the delayed worker's idle stream), a sample with a longer round trip is
-// dropped, and the rate is measured over at least kClockRateSpanNs
+// the host <-> device clock map behind device deadlines is refreshed this often by a sampling
+// thread of its own (one probe round trip on a stream of its own: never on the coordinator's
+// path -- a probe taken inside a call cost kmap2_n9 a 1.4 ms harvest hop, r06d), a sample with a
+// longer round trip is dropped, and the rate is measured over at least kClockRateSpanNs
 constexpr uint64_t kClockRecalNs = 250000000;
 constexpr int64_t kClockMaxRttNs = 40000;
 constexpr int64_t kClockRateSpanNs = 1000000000;
@@ -303,26 +304,24 @@ class HipComm final : public Comm {
   // epoch's batched launch instead of alone before it (c5, nwait 7 of 8: one 8-task launch
   // per epoch instead of a 1-task launch and a 7-task launch, profiles/r02_c5_hold_ab.txt).
   // The pool's state machine is unchanged; MPA_HOLD=0 launches re-dispatches at once.
-  // Only while another task of this process is still running does holding pay: with nothing
-  // local in flight (rank 0 of the node's placement, whose one local worker is the stale one)
-  // the held task would only start one epoch late, so it launches at once (r06b).
+  // Holding pays only where the held task has a batch to join: another local undelayed
+  // least-squares worker of this process.  Rank 0 of the node's placement serves one worker, the
+  // stale one itself: held, its task would only start an epoch late (r06b), so it launches at
+  // once.  (Where peers exist the hold stays whether or not they are still running: c1's
+  // whole-pool pre-armed launches depend on the held task joining the next one, -18 % in r06d.)
   void flush_stale() override {
-    hold_next_ = hold_ok_ && local_in_flight();
+    hold_next_ = hold_ok_ && has_batch_peer();
     flush();
     hold_next_ = false;
   }
-  // a local undelayed least-squares worker (its tasks run in the batches a held task joins)
-  // other than the ones this flush posts has a launched task not yet seen done
-  bool local_in_flight() const {
+  // a local undelayed least-squares worker other than the ones this flush posts
+  bool has_batch_peer() const {
     for (int64_t r = 1; r <= nworkers_; ++r) {
       const HipWorker& w = w_[size_t(r - 1)];
       const TaskSpec& ts = tasks_[size_t(r - 1)];
-      if (!w.here || w.remote || w.seq == 0 || !ts.delays_ns.empty() ||
-          (ts.kind != MPA_TASK_LSQ && ts.kind != MPA_TASK_LSQ_BATCH) || done(r))
+      if (!w.here || w.remote || !ts.delays_ns.empty() || (ts.kind != MPA_TASK_LSQ && ts.kind != MPA_TASK_LSQ_BATCH))
         continue;
-      if (std::find(posts_.begin(), posts_.end(), r) != posts_.end()) continue;
-      if (std::find(held_.begin(), held_.end(), r) != held_.end()) continue;
-      return true;
+      if (std::find(posts_.begin(), posts_.end(), r) == posts_.end()) return true;
     }
     return false;
   }
@@ -945,14 +944,24 @@ class HipComm final : public Comm {
   bool caller_null_ = true;                // the caller's stream (set_stream) is the NULL stream
   int64_t delay_lead_ns_ = kDelayLeadNs;   // MPA_DELAY_LEAD_NS: the timer's launch overhead, out of its sleep
   int64_t deadline_lead_ns_ = kDeadlineLeadNs;
-  // host <-> device clock map (steady-clock ns, s_memrealtime ticks): the first sample and the latest
+  // host <-> device clock map (steady-clock ns, s_memrealtime ticks): the first sample and the
+  // latest (ck_mu_: the sampling thread writes them)
   int64_t ck_t0_ = 0, ck_n0_ = 0, ck_t1_ = 0, ck_n1_ = 0;
-  int64_t n_clock_samples_ = 0;
+  std::atomic<int64_t> n_clock_samples_{0};
+  std::mutex ck_mu_;
+  std::mutex tmu_ck_;  // the sampling thread's sleep / stop
+  std::thread ck_thread_;
+  std::condition_variable ck_cv_;
+  bool ck_stop_ = false;
+  hipStream_t ck_stream_ = nullptr;
+  uint64_t* ck_probe_ = nullptr;  // host-pinned word the clock probes store into
   bool device_delay_ok(hipStream_t s) const;
-  unsigned long long device_deadline(int64_t host_ns, hipStream_t s);
+  unsigned long long device_deadline(int64_t host_ns);
   // one probe round trip on `s` (idle): (device ticks, host ns) at its midpoint, returns the round
   // trip in ns (or -1: the probe had not landed after 100 ms)
   int64_t clock_sample(hipStream_t s, int64_t* ticks, int64_t* ns);
+  void clock_loop();
+  void stop_clock();
   int64_t n_sleeps_ = 0;  // delayed tasks queued behind a device deadline
   int64_t n_armed_ = 0;   // server: tasks launched device-armed (counter 'armed')  // delayed tasks (a sleep kernel before the task, counter 'sleeps')
 

@@ -180,6 +180,7 @@ HipComm::~HipComm() {
   } catch (...) {
   }
   stop_timer();
+  stop_clock();
   (void)hipDeviceSynchronize();
 #if MPA_MEASURE
   if (const char* d = measure_env("MPA_LSQF_DBG"); d && (std::atoi(d) & 16)) lsqf_prof_dump();
@@ -218,6 +219,8 @@ HipComm::~HipComm() {
   if (cancel_) (void)hipHostFree(cancel_);
   if (trace_) (void)hipHostFree(trace_);
   if (clock_probe_) (void)hipHostFree(clock_probe_);
+  if (ck_probe_) (void)hipHostFree(ck_probe_);
+  if (ck_stream_) (void)hipStreamDestroy(ck_stream_);
   if (pre_mb_) {
     cancel_pre();
     (void)hipStreamSynchronize(coord_);  // the cancelled launch has left before its mailbox goes
@@ -528,7 +531,7 @@ void HipComm::on_delays_changed(int64_t rank) {
   HipWorker& w = w_[size_t(rank - 1)];
   if (!w.here || tasks_[size_t(rank - 1)].delays_ns.empty()) return;
   hipStream_t s = worker_stream(w);
-  if (ck_n0_) return;
+  if (ck_thread_.joinable()) return;
   int64_t best = INT64_MAX;
   for (int k = 0; k < 16; ++k) {
     int64_t t = 0, n = 0;
@@ -541,6 +544,9 @@ void HipComm::on_delays_changed(int64_t rank) {
   }
   if (best == INT64_MAX) fail(MPA_DEVICE_ERROR, "clock calibration: no probe landed");
   n_clock_samples_ = 1;
+  HIPCHECK(hipStreamCreateWithFlags(&ck_stream_, hipStreamNonBlocking));
+  ck_stop_ = false;
+  ck_thread_ = std::thread([this]() { clock_loop(); });
 }
 
 void HipComm::launch_local(const std::vector<int64_t>& posted) {
@@ -842,7 +848,7 @@ int64_t HipComm::counter(const char* name) const {
   if (k == "prearm_same") return n_pre_same_;  // released with the step's predicted arguments
   if (k == "armed") return n_armed_;  // server: tasks launched device-armed (some may be cancelled)
   if (k == "sleeps") return n_sleeps_;  // delayed tasks queued behind a device deadline (deadline_kernel)
-  if (k == "clock_samples") return n_clock_samples_;  // host <-> device clock samples behind the deadlines
+  if (k == "clock_samples") return n_clock_samples_.load(std::memory_order_relaxed);  // host <-> device clock samples behind the deadlines
   if (k == "timer_late") return n_timer_late_.load(std::memory_order_relaxed);  // > 1 ms late timer launches
   if (k == "queues") return queue_streams(dev_);  // CU-masked streams (HSA queues) the process holds
   if (k == "shared_worker_streams") {  // workers whose stream another worker or comm also uses
