@@ -9,6 +9,7 @@
 // program order makes a deferred copy observable (before a worker's irecv chunk can be
 // overwritten) and end_call() before returning to the caller.
 #pragma once
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <thread>
@@ -20,18 +21,24 @@
 namespace mpa {
 
 // A polite poll for the transport's long waits: pause for the first kHotSpinNs of a wait (c1's
-// epochs wait microseconds: no system call on that path), then yield the core on every poll.  The
-// coordinator's wait and the straggler timer's final spin are two busy threads of one process; on
-// a core they share, a bare pause loop keeps the other one off until the scheduler's time slice
-// ends.  (Sleeping between polls instead -- 20 us asked, ~60 us of timer slack got -- moved the
-// gated replays' median harvest from 4 to 42 us and their worst from 1.0 to 1.5 ms: r05o.)
+// epochs wait microseconds: no system call on that path), then yield the core on every poll --
+// while a straggler timer of this process has a launch pending.  The coordinator's wait and the
+// timer's final spin are two busy threads of one process; on a core they share, a bare pause loop
+// keeps the other one off until the scheduler's time slice ends.  With no timer work (delays as
+// device deadlines, or none) the wait keeps pausing: on a loaded box (loadavg 20+) a yield gave
+// the core away for a slice and the gated kmap2_n9 replay harvested 1.0-1.4 ms late (r06d, r06e).
+// A worker process's idle doorbell poll always yields once cold (yield_cold).  (Sleeping between
+// polls instead -- 20 us asked, ~60 us of timer slack got -- moved the gated replays' median
+// harvest from 4 to 42 us and their worst from 1.0 to 1.5 ms: r05o.)
 constexpr int64_t kHotSpinNs = 50000;
+extern std::atomic<int64_t> g_timer_pending;  // host-timer launches pending in this process
 struct PoliteSpin {
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   uint32_t n = 0;
   bool cold = false;
+  bool yield_cold = false;  // yield once cold whether or not a timer is pending
   void operator()() {
-    if (cold) {
+    if (cold && (yield_cold || g_timer_pending.load(std::memory_order_relaxed) > 0)) {
       std::this_thread::yield();
       return;
     }

@@ -1,8 +1,12 @@
+#include <atomic>
+
+#include "comm.hpp"
 #include "common.hpp"
 
 namespace mpa {
 
 static thread_local std::string g_err;
+std::atomic<int64_t> g_timer_pending{0};
 
 void set_error(const char* fmt, ...) {
   char buf[1024];

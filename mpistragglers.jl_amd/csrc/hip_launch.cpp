@@ -419,6 +419,7 @@ void HipComm::defer(uint64_t due, std::function<void()> go) {
   }
   deferred_.push_back(Deferred{due, std::move(go)});
   std::push_heap(deferred_.begin(), deferred_.end());
+  g_timer_pending.fetch_add(1, std::memory_order_relaxed);
   tfront_.store(deferred_.front().due, std::memory_order_release);
   tcv_.notify_all();
 }
@@ -459,6 +460,7 @@ void HipComm::timer_loop() {
     std::pop_heap(deferred_.begin(), deferred_.end());
     Deferred d = std::move(deferred_.back());
     deferred_.pop_back();
+    g_timer_pending.fetch_sub(1, std::memory_order_relaxed);
     tfront_.store(deferred_.empty() ? ~0ull : deferred_.front().due, std::memory_order_release);
     tbusy_ = true;
     lk.unlock();
@@ -481,6 +483,7 @@ void HipComm::stop_timer() {
     std::lock_guard<std::mutex> lk(tmu_);
     tstop_ = true;
     tstop_spin_.store(true, std::memory_order_release);
+    g_timer_pending.fetch_sub(int64_t(deferred_.size()), std::memory_order_relaxed);
     deferred_.clear();
     tfront_.store(~0ull, std::memory_order_release);
     tcv_.notify_all();

@@ -16,6 +16,7 @@ void HipComm::serve() {
   } disarm_guard{this};
   std::vector<int64_t> fresh;
   PoliteSpin idle;  // the doorbell poll between tasks (hot for kHotSpinNs, then yielding)
+  idle.yield_cold = true;
   for (int64_t r = 1; r <= nworkers_; ++r)
     if (w_[size_t(r - 1)].here && server_path(r) && armable(r)) arm(r);
   for (uint64_t spins = 0;; ++spins) {
@@ -89,11 +90,13 @@ void HipComm::serve() {
       if (timing_) reap_timing(false);
       launch_tasks(fresh, /*staged=*/true);
       idle = PoliteSpin{};
+      idle.yield_cold = true;
     } else if (!progress) {
       if ((spins & 0xFFF) == 0xFFF) watchdog(t0, /*timeout=*/false);
       idle();
     } else {
       idle = PoliteSpin{};  // busy again: the next idle stretch starts hot
+      idle.yield_cold = true;
     }
   }
 }

@@ -795,6 +795,7 @@ hipError_t launch_lsq(int dtype, int cols, const LsqBatch& a, hipStream_t s) {
           case 3: return go<float, 8, 2, kMode | M_PREFETCH>(a, s);
           case 4: return go<float, 8, 1, kMode | M_PREFETCH>(a, s);
           case 5: return go<float, 8, 2, kMode | M_BLOCKED>(a, s);
+          case 6: return go<float, 8, 4, kMode | M_BLOCKED>(a, s);
           default: break;
         }
 #endif
