@@ -232,14 +232,15 @@ def kernel_name(cfg):
     return "lsq_grad_kernel (one batched launch per epoch per GPU)"
 
 
-def read_peak(M, torch):
+def read_peak(M, torch, nbytes=1 << 32):
     """Measured HBM read ceiling of this GPU (mpa_read_bandwidth): a plain non-temporal
-    streaming read of a 4 GiB buffer at three grid sizes, best of them, outside the timed
-    region.  Reported beside the spec peak so the roofline fraction can be read against
-    what a read-only kernel reaches on the same box."""
-    buf = torch.empty(1 << 30, dtype=torch.float32, device="cuda")
+    streaming read of a 4 GiB buffer (or `nbytes`: one launch's bytes of a per-GPU measurement
+    config) at four grid sizes, best of them, outside the timed region.  Reported beside the spec
+    peak so the roofline fraction can be read against what a read-only kernel reaches on the same
+    box."""
+    buf = torch.empty(int(nbytes) // 4, dtype=torch.float32, device="cuda")
     buf.fill_(1.0)
-    best = max(M.read_bandwidth(buf, grid=g, reps=10) for g in (512, 1024, 2048, 4096))
+    best = max(M.read_bandwidth(buf, grid=g, reps=10) for g in (192, 512, 1024, 2048, 4096))
     del buf
     torch.cuda.empty_cache()
     return round(best, 1)
@@ -372,6 +373,10 @@ def report(args, cfg, world, el, per_rank, extra):
     if rp:
         out["roofline"]["measured_read_peak"] = rp
         out["roofline"]["frac_of_measured_read_peak"] = round(achieved / rp, 4) if achieved else None
+    rpl = extra.pop("measured_read_peak_launch_bytes", None)
+    if rpl:
+        out["roofline"]["measured_read_peak_launch_bytes"] = rpl
+        out["roofline"]["frac_of_measured_read_peak_launch_bytes"] = round(achieved / rpl, 4) if achieved else None
     out.update(extra)
     return out
 
@@ -532,6 +537,10 @@ def run_single(args, cfg):
     comm.timing()
     comm.set_timing(False)
     extra["measured_read_peak"] = read_peak(M, torch)
+    if timing[0] and timing[2] / timing[0] < 3.5e9:
+        # a launch smaller than the 4 GiB probe (the per-GPU shares c2n2 / c2n4 / c2n8): the
+        # same read at that size, whose ramp and tail weigh as they do in the launch
+        extra["measured_read_peak_launch_bytes"] = read_peak(M, torch, timing[2] / timing[0] // 4096 * 4096)
     extra.update({"x_norm": float(torch.linalg.norm(x.float()).item()), "build": M.lib().mpa_build_info().decode(),
                   "loop": "native coordinator loop (mpa_lsq%s_descent)" % ("b" if batched else ""),
                   "fresh_at_last_epoch": fresh})

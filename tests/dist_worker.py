@@ -549,27 +549,29 @@ def lsq_sched_dist(rank, world, port, placement, config, epoch0, result_q):
 
 # The native k-of-n loop across processes: what bench.py's rank 0 runs at
 # N > 1 for c3 / c4 / c5 (make_loop: mpa_lsq_descent / mpa_lsqb_descent on a DistComm).  Worker 1
-# lives on rank 0; `rows` makes it the slow one (an undelayed local task: its stale reply and its
-# re-dispatch, src/MPIAsyncPools.jl:177-184), the remote workers carry Exp(delay_ms) injected
-# delays (their stale replies are harvested from other processes' GPUs).  eta keeps the slow
-# worker's gradient from converging towards zero over the run (its own L = rows / (3 cols) is
-# large): a gradient that cancels down to its rounding has no relative accuracy left to check.
+# lives on rank 0 and is made the straggler -- c3 by an injected 3 ms delay per task, c5 by a shard
+# 4096x the others' (an undelayed task: the kind a stale re-dispatch may hold) -- so its stale
+# replies and re-dispatches (src/MPIAsyncPools.jl:177-184) happen every few epochs; remote workers
+# carry injected delays (`remote`: Exp(mean ms) per task, or "spikes": 3 ms every 4th task of the
+# last worker, none for the others), their stale replies harvested from other processes' GPUs.
+# eta keeps the slow worker's gradient from converging towards zero over the run (its own L =
+# rows / (3 cols) is large): a gradient that cancels down to its rounding has no relative accuracy
+# left to check.
 KOFN_CONFIGS = {
     # c3: fp32, nwait 6 of 8, stale results dropped; the node's placement (rank 0 serves worker
     # 1 only), so worker 1's stale re-dispatch launches at once (nothing else of rank 0's runs)
     "c3": dict(dt="f32", cols=2048, nwait=6, stale=0.0, tol=1e-5, placement=list(range(8)),
-               rows=[1 << 21] + [256] * 7, delay_ms=0.1, epochs=40, eta=2e-5),
+               rows=[256] * 8, local_delay_ms=3.0, remote=0.1, epochs=40, eta=0.05),
     # c4: fp64, worker 1 fresh + 5 others (first_plus), stale results at weight 0.5; worker 1 fast
     "c4": dict(dt="f64", cols=2048, nwait="first_plus5", stale=0.5, tol=1e-12, placement=list(range(8)),
-               rows=[256] * 8, delay_ms=1.0, epochs=40, eta=0.05),
+               rows=[256] * 8, local_delay_ms=None, remote=1.0, epochs=40, eta=0.05),
     # c5: the batched 64-iterate variant (bf16 messages, fp32 accumulate), nwait 7 of 8; rank 0
-    # serves workers 1 (slow: ~1 ms) and 2 (fast), so nwait can be met without worker 1 (and the
-    # remote Exp(0.4 ms) delays now and then exceed it: remote stale replies too); worker
-    # 2's next task queues behind worker 1's running launch on the coordinator stream, so worker
-    # 1's stale re-dispatch is HELD and joins worker 2's next launch; eta small enough that G
-    # never cancels down to its rounding (bf16 messages)
+    # serves workers 1 (slow: ~1 ms of lsqp4) and 2 (fast); worker 2's next task queues behind
+    # worker 1's running launch on the coordinator stream, so worker 1's stale re-dispatch is
+    # HELD and joins worker 2's next launch; the last worker's 3 ms spikes make it the stale one
+    # now and then
     "c5": dict(dt="bf16", cols=2048, nwait=7, stale=0.0, tol=1e-5, placement=[0, 0, 1, 2, 3, 4, 5, 6],
-               rows=[1 << 20] + [256] * 7, delay_ms=0.4, epochs=30, eta=2e-5, k=64),
+               rows=[1 << 20] + [256] * 7, local_delay_ms=None, remote="spikes", epochs=30, eta=2e-5, k=64),
 }
 
 
@@ -626,9 +628,14 @@ def descent_kofn_dist(rank, world, port, config, epoch0, result_q):
                 comm.set_task_lsq_batch(w, *keep[-1])
             else:
                 comm.set_task_lsq(w, *keep[-1])
-            if rank != 0:
+            if rank == 0 and cfg["local_delay_ms"]:
+                comm.set_delays(w, [int(cfg["local_delay_ms"] * 1e6)])
+            elif rank != 0 and cfg["remote"] == "spikes":
+                if w == n:
+                    comm.set_delays(w, [0, 0, 0, 3_000_000])
+            elif rank != 0:
                 rng = np.random.default_rng([17, w])
-                comm.set_delays(w, rng.exponential(cfg["delay_ms"] * 1e6, size=512).astype(np.int64))
+                comm.set_delays(w, rng.exponential(cfg["remote"] * 1e6, size=512).astype(np.int64))
         torch.cuda.synchronize()
         dist.barrier()
         if rank != 0:

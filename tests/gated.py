@@ -297,8 +297,16 @@ def explain_misses(got, trace, bad):
         mine = [e for e in trace if e[F["rank"]] == rank and t0 <= e[F["harvest"]] <= t1]
         during = [e for e in trace if e[F["seen"]] and t0 <= e[F["seen"]] <= t1 and e[F["pub"]]]
         worst = max(during, key=lambda e: e[F["pub"]] - e[F["due"]], default=None)
+        # the coordinator's activity before the late harvest: every task posted, launched or
+        # harvested in the 3 ms before it (ms relative to the harvest)
+        h = mine[-1][F["harvest"]] if mine else t1
+        rel = lambda v: round((v - h) / 1e6, 3) if v else None  # noqa: E731
+        near = [e for e in trace if any(h - 3_000_000 <= e[F[f]] <= h for f in ("post", "call", "harvest", "pub"))]
+        act = [{"task": "r%d#%d" % (e[F["rank"]], e[F["seq"]]), "post": rel(e[F["post"]]), "call": rel(e[F["call"]]),
+                "ret": rel(e[F["ret"]]), "pub": rel(e[F["pub"]]), "seen": rel(e[F["seen"]]), "harvest": rel(e[F["harvest"]])}
+               for e in sorted(near, key=lambda e: e[F["post"]])][-8:]
         out.append({"op": k, "pos": i, "dev_ms": d, "harvested": task_parts(mine[-1]) if mine else None,
-                    "latest_in_call": task_parts(worst) if worst is not None else None})
+                    "latest_in_call": task_parts(worst) if worst is not None else None, "activity": act})
     return out
 
 
