@@ -878,12 +878,7 @@ void HipComm::enqueue_lsqb(const LsqbLaunch& b, hipStream_t s, double bytes, int
     HIPCHECK(hipEventRecord(tl.start, s));
   }
 #if MPA_MEASURE
-  static const bool p5 = [] { const char* e = measure_env("MPA_LSQP5"); return e && *e == '1'; }();
-  static const bool p6 = [] { const char* e = measure_env("MPA_LSQP6"); return e && *e == '1'; }();
-  static const bool p7 = [] { const char* e = measure_env("MPA_LSQP7"); return e && *e == '1'; }();
-  HIPCHECK(b.pair ? (b.cpair ? launch_lsqc(b.halves, s) : b.pair8 ? launch_lsqp(b.halves, s)
-                             : p7 ? launch_lsqp7(b.halves, s) : p6 ? launch_lsqp6(b.halves, s)
-                             : p5 ? launch_lsqp5(b.halves, s) : launch_lsqp4(b.halves, s))
+  HIPCHECK(b.pair ? (b.cpair ? launch_lsqc(b.halves, s) : b.pair8 ? launch_lsqp(b.halves, s) : launch_lsqp4(b.halves, s))
                   : b.quad ? launch_lsqq(b.four, s) : b.fused ? launch_lsqf(b.one, s) : launch_lsqb(b.two, s));
 #else
   // the product carries the iterate-halves single pass and the two passes only

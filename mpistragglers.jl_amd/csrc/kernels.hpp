@@ -290,17 +290,9 @@ struct LsqpBatch {
 hipError_t launch_lsqp(const LsqpBatch& a, hipStream_t s);
 // the same batch by the one-wave-per-SIMD cut (lsqp4_kernel.hip, the default)
 hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s);
-// the same with phase 2 as 32x32x16 MFMAs (measure/lsqp5_kernel.hip, measurement build: MPA_LSQP5=1;
-// fewer instructions, the same time: DESIGN.md §10)
-hipError_t launch_lsqp5(const LsqpBatch& a, hipStream_t s);
-// lsqp4 software-pipelined across blocks: phase 1 of block v beside phase 2 of block v - 1
-// (measure/lsqp6_kernel.hip, measurement build: MPA_LSQP6=1; bitwise equal to lsqp4, 23 % faster
-// with L2-hot loads, equal streaming A from HBM: DESIGN.md §10)
-hipError_t launch_lsqp6(const LsqpBatch& a, hipStream_t s);
-// lsqp4 by pairs of 16-row blocks: phase 2 over the pair's 32 distinct rows, hi and lo as two
-// MFMAs, half the transposed LDS reads (measure/lsqp7_kernel.hip, measurement build: MPA_LSQP7=1;
-// FULL batches, others go to lsqp4)
-hipError_t launch_lsqp7(const LsqpBatch& a, hipStream_t s);
+// (rounds 4-5 measured three more restructurings of lsqp4 -- phase 2 as 32x32x16 MFMAs, the
+// block-pipelined kernel, the pair step -- parity-green and level with it on HBM; removed in round
+// 6, their record is DESIGN.md §10 and profiles/r04_c5_*, r05_c5_pairstep.txt)
 // Single pass by COLUMN pairs (lsqc_kernel.hip): the two members of a row group split the
 // columns (member h: columns 1024 h .. 1024 h + 1023), each holding all 64 iterates of its G
 // columns, and exchange their 16 x 64 partial products per 16-row block as tagged granules.

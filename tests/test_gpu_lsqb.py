@@ -277,77 +277,3 @@ for rows, cols, n, seed in T._VARIANT_CASES:
 np.savez(sys.argv[2], *outs)
 """
 _VARIANT_CASES = [(4800, 2048, 2, 91), (3001, 2048, 3, 92), (2500, 1312, 2, 93)]
-
-
-@pytest.mark.parametrize("var", ["MPA_LSQP6"])
-def test_pipelined_variant_matches_lsqp4_bitwise(M, tmp_path, var):
-    """The software-pipelined c5 kernel (measure/lsqp6_kernel.hip, measurement build,
-    MPA_LSQP6=1: phase 1 of block v beside phase 2 of block v - 1) sums in lsqp4's order (the
-    -B MFMA, k-steps in order, the same reduce, the blocks in order; block -1 adds an exact
-    +0), so its G equals lsqp4's bit for bit, FULL (cols 2048, rows % 16 = 0) and general form.
-    The variant is chosen once per process (a static read of the environment): it runs in a
-    child process on the same inputs."""
-    import os
-    import subprocess
-    import sys
-    import torch
-    if b"measurement build" not in M.lib().mpa_build_info():
-        pytest.skip("a c5 variant of the measurement build (make MEASURE=1, MPA_LIB=...): not in the product")
-    if os.environ.get(var):
-        pytest.skip(f"{var} is set for this process: lsqp4 is not the in-process kernel")
-    mine = []
-    for rows, cols, n, seed in _VARIANT_CASES:
-        A, B, X = _problem(n * rows, cols, seed)
-        shards = [(A[i * rows:(i + 1) * rows - (i if rows % 16 else 0)], B[i * rows:(i + 1) * rows - (i if rows % 16 else 0)])
-                  for i in range(n)]
-        out, rep, comm, _ = _run(M, torch, shards, cols, X)
-        comm.close()
-        mine.append(out)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    dst = str(tmp_path / "variant.npz")
-    env = dict(os.environ, **{var: "1"})
-    subprocess.run([sys.executable, "-c", _VARIANT_CHILD, root, dst], env=env, check=True, timeout=180)
-    theirs = np.load(dst)
-    for k, out in enumerate(mine):
-        assert np.array_equal(out.view(np.uint32), theirs[f"arr_{k}"].view(np.uint32)), _VARIANT_CASES[k]
-
-
-_PAIR_CASES = [(4800, 2048, 2, 91), (4816, 2048, 2, 94), (16, 2048, 1, 95), (48, 2048, 3, 96), (3001, 2048, 3, 92)]
-
-
-def test_pair_step_variant_vs_oracle(M, tmp_path):
-    """The pair-step c5 kernel (measure/lsqp7_kernel.hip, measurement build, MPA_LSQP7=1: phase 2
-    over two blocks' 32 distinct rows, hi and lo as two MFMAs, half the transposed reads) against
-    the oracle at 1e-5 on FULL shards with even and odd block counts per row group (a pair past
-    the range's end adds a zero residual), one block, three tasks per launch, and a general-form
-    batch that it hands to lsqp4; within 1e-6 of lsqp4 (regrouped sums, not bitwise).  Chosen once
-    per process: it runs in a child process on the same inputs."""
-    import os
-    import subprocess
-    import sys
-    import lsq
-    import torch
-    if b"measurement build" not in M.lib().mpa_build_info():
-        pytest.skip("a c5 variant of the measurement build (make MEASURE=1, MPA_LIB=...): not in the product")
-    if os.environ.get("MPA_LSQP7"):
-        pytest.skip("MPA_LSQP7 is set for this process: lsqp4 is not the in-process kernel")
-    mine, probs = [], []
-    for rows, cols, n, seed in _PAIR_CASES:
-        A, B, X = _problem(n * rows, cols, seed)
-        shards = [(A[i * rows:(i + 1) * rows - (i if rows % 16 else 0)], B[i * rows:(i + 1) * rows - (i if rows % 16 else 0)])
-                  for i in range(n)]
-        out, rep, comm, _ = _run(M, torch, shards, cols, X)
-        comm.close()
-        mine.append(out)
-        probs.append((shards, X))
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    dst = str(tmp_path / "pair.npz")
-    child = _VARIANT_CHILD.replace("T._VARIANT_CASES", "T._PAIR_CASES")
-    subprocess.run([sys.executable, "-c", child, root, dst], env=dict(os.environ, MPA_LSQP7="1"), check=True, timeout=180)
-    theirs = np.load(dst)
-    for k, (out, (shards, X)) in enumerate(zip(mine, probs)):
-        got = theirs[f"arr_{k}"]
-        for i, (Ai, Bi) in enumerate(shards):
-            err = lsq.rel_err(got[i], lsq.batched_shard_gradient(Ai, Bi, X, "bf16"))
-            assert err <= TOL, (_PAIR_CASES[k], i, err)
-            assert lsq.rel_err(got[i], out[i]) <= 1e-6, (_PAIR_CASES[k], i)
