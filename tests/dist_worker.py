@@ -764,8 +764,14 @@ def descent_kofn_dist(rank, world, port, config, epoch0, result_q):
             errors.append(("held a re-dispatch with nothing else of rank 0's in flight", got))
         if config == "c5" and not (got["held"] >= 1 and got["held_joined"] >= 1):
             errors.append(("no held re-dispatch joined a launch", got))
-        print("descent k-of-n %s epoch0 %d: %s, stale harvests local %d remote %d, iterate rel %.2e"
-              % (config, epoch0, got, stale_local, stale_remote, rel), flush=True)
+        lat = [list(map(float, m.group(1).split()))
+               for m in re.finditer(r"\| latency ms ([\d. ]+)\n", err)]
+        med_lat = [round(float(np.median([row[i] for row in lat])), 2) for i in range(n)] if lat else None
+        print("descent k-of-n %s epoch0 %d: %s, stale harvests local %d remote %d, iterate rel %.2e, "
+              "median latency per worker (ms) %s" % (config, epoch0, got, stale_local, stale_remote, rel, med_lat),
+              flush=True)
+        if errors:
+            errors.append(("median latency per worker (ms)", med_lat))
         result_q.put(("ok", errors))
     except Exception:
         result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
