@@ -101,18 +101,22 @@ void HipComm::serve() {
   }
 }
 
-// Device-armed tasks: least-squares workers without injected delays whose
-// messages arrive in this GPU's slot (device payload path).  MPA_ARM: 0 never, 1 every such
-// worker, 2 (default) where the process serves one worker (the N = 8 placement; a process
-// with several workers launches the tasks of a flush as one batch instead).  The in-kernel
-// wait (MPA_ARM_WAIT=kernel: every workgroup of the armed launch waits) is refused by the
-// default on a GPU that rank 0 also uses: the waiting grids held the CUs rank 0's kernels
-// needed to ring them (profiles/r03_rehearsal_n248.txt); the default one-wave
-// wait (door_wait_kernel) holds nothing anyone needs.
+// Device-armed tasks: least-squares workers whose messages arrive in this GPU's
+// slot (device payload path).  MPA_ARM: 0 never, 1 every such worker, 2 (default) where the
+// process serves one worker (the N = 8 placement; a process with several workers launches the
+// tasks of a flush as one batch instead).  The in-kernel wait (MPA_ARM_WAIT=kernel: every
+// workgroup of the armed launch waits) is refused by the default on a GPU that rank 0 also uses:
+// the waiting grids held the CUs rank 0's kernels needed to ring them
+// (profiles/r03_rehearsal_n248.txt); the default one-wave wait (door_wait_kernel)
+// holds nothing anyone needs.  A worker with injected delays is armed too (round 6), behind the
+// one-wave wait, which sleeps its delay from the ring on the device: host-launched, its delay
+// began only when this process's serve loop saw the doorbell -- milliseconds late on a loaded
+// box, when a yielding poll lost its core (the one-GPU k-of-n process tests, r06h).
 bool HipComm::armable(int64_t rank) const {
   const TaskSpec& ts = tasks_[size_t(rank - 1)];
   const HipWorker& w = w_[size_t(rank - 1)];
-  if (arm_mode_ == 0 || !w.path_dev || !((ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) && ts.delays_ns.empty()))
+  if (arm_mode_ == 0 || !w.path_dev || !(ts.kind == MPA_TASK_LSQ || ts.kind == MPA_TASK_LSQ_BATCH) ||
+      (!ts.delays_ns.empty() && (!arm_wave_ || delay_mode_ == 1)))
     return false;
   if (arm_mode_ == 1) return true;
   int here = 0;
@@ -142,7 +146,13 @@ void HipComm::arm(int64_t rank) {
   w.out = reply_dst(w);
   hipStream_t st = worker_stream(w);
   unsigned long long* door = arm_wave_ ? nullptr : own_door(w);
-  if (arm_wave_) HIPCHECK(launch_door_wait(own_door(w), s, spin_ticks(), err_dev_, w.cancel_dev, st));
+  // the injected delay of task s (launch_tasks' schedule index), less the overhead that follows
+  // the wait: the task's dispatch behind it, the task, its completion word
+  const int64_t delay = ts.delays_ns.empty() ? 0 : ts.delays_ns[size_t((int64_t(s) - 1) % int64_t(ts.delays_ns.size()))];
+  const int64_t sleep_ns = delay - deadline_lead_ns_;
+  const unsigned long long sleep_ticks = sleep_ns > 0 ? (unsigned long long)(double(sleep_ns) * rt_hz_ / 1e9) : 0ull;
+  if (sleep_ticks) n_sleeps_ += 1;
+  if (arm_wave_) HIPCHECK(launch_door_wait(own_door(w), s, spin_ticks(), err_dev_, w.cancel_dev, sleep_ticks, st));
   double bytes = 0;
   if (ts.kind == MPA_TASK_LSQ) {
     LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes, armed_share());

@@ -281,38 +281,46 @@ hipError_t launch_door_cas(unsigned long long* door, unsigned long long expect, 
 // on a message rank 0 never posted.
 __global__ void __launch_bounds__(64) door_wait_kernel(const unsigned long long* door, unsigned long long seq,
                                                        unsigned long long spin_ticks, unsigned* err,
-                                                       unsigned long long* cancel) {
+                                                       unsigned long long* cancel, unsigned long long delay_ticks) {
   if (threadIdx.x) return;
   const unsigned long long t0 = rt_now();
-  for (unsigned k = 0; (__hip_atomic_load(door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & ~kCancelBit) < seq; ++k) {
+  unsigned long long d = 0;
+  for (unsigned k = 0; ((d = __hip_atomic_load(door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) & ~kCancelBit) < seq;
+       ++k) {
     __builtin_amdgcn_s_sleep(2);
     if ((k & 255) == 255 && rt_now() - t0 > spin_ticks) {
       __hip_atomic_store(cancel, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_fetch_or(err, 64u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      d = kCancelBit;
       break;
     }
+  }
+  // a delayed worker (an injected straggler, test/kmap2.jl:95's sleep between its Irecv and its
+  // reply) sleeps from the moment its doorbell rang, here on the device: no host thread between
+  // the ring and the task (a cancelled task -- pause / shutdown -- does not sleep)
+  if (delay_ticks && !(d & kCancelBit)) {
+    const unsigned long long t1 = rt_now();
+    while (rt_now() - t1 < delay_ticks) __builtin_amdgcn_s_sleep(2);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the message the doorbell released
 }
 
 hipError_t launch_door_wait(const unsigned long long* door, unsigned long long seq, unsigned long long spin_ticks,
-                            unsigned* err, unsigned long long* cancel, hipStream_t s) {
+                            unsigned* err, unsigned long long* cancel, unsigned long long delay_ticks, hipStream_t s) {
   if (!door || !err || !cancel) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(door_wait_kernel, dim3(1), dim3(64), 0, s, door, seq, spin_ticks, err, cancel);
+  hipLaunchKernelGGL(door_wait_kernel, dim3(1), dim3(64), 0, s, door, seq, spin_ticks, err, cancel, delay_ticks);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------
-// Straggler emulation: a delayed worker's task runs on its own stream behind
-// this one-wave kernel, which starts once the worker's message has landed (stream order after
-// the exchange) and spins on s_memrealtime for the injected delay -- the reference worker's
-// sleep(rand()) between its Irecv and its reply (examples/iterative_example.jl:74,
-// test/kmap2.jl:95).  No host thread sits between the schedule and the latency the pool
-// records; one wave holds no CU anyone else needs.
-// An injected straggler delay on the device: one wave waits on its worker's stream, ahead of
-// the task, until an ABSOLUTE deadline on the GPU's constant 100 MHz clock (the host's post time
-// + the delay, mapped through the clock calibration, HipComm::device_deadline): when the stream
-// reaches it does not matter, and no host thread has to wake up on time.  Bounded (err bit 256).
+// Straggler emulation: the reference worker sleeps rand() between its Irecv and
+// its reply (examples/iterative_example.jl:74, test/kmap2.jl:95).  A delayed worker of the
+// coordinator's process waits on its worker's stream, ahead of the task, in this one-wave
+// kernel until an ABSOLUTE deadline on the GPU's constant 100 MHz clock (the host's post time +
+// the delay, mapped through the clock calibration, HipComm::device_deadline): when the stream
+// reaches it does not matter, no host thread has to wake up on time, one wave holds no CU anyone
+// else needs.  Bounded (err bit 256).  (A device-armed worker of another process sleeps inside
+// its door_wait_kernel instead, from its doorbell.)
 __global__ void __launch_bounds__(64) deadline_kernel(unsigned long long deadline, unsigned long long bound,
                                                        unsigned* err) {
   if (threadIdx.x) return;

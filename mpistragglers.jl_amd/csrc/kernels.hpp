@@ -384,9 +384,10 @@ hipError_t launch_clock_probe(unsigned long long* out, hipStream_t s);
 hipError_t launch_kmap(const KmapArgs& a, hipStream_t s);
 // one wave that waits for a device-armed task's doorbell (seq, with or without kCancelBit;
 // bounded by spin_ticks: on timeout it stores seq into `cancel`, the queued task's go word, so
-// the task cancels itself, and sets err bit 64), then acquires at system scope; the task runs behind it
+// the task cancels itself, and sets err bit 64), then -- a delayed worker, not cancelled -- sleeps
+// delay_ticks from the ring, then acquires at system scope; the task runs behind it
 hipError_t launch_door_wait(const unsigned long long* door, unsigned long long seq, unsigned long long spin_ticks,
-                            unsigned* err, unsigned long long* cancel, hipStream_t s);
+                            unsigned* err, unsigned long long* cancel, unsigned long long delay_ticks, hipStream_t s);
 // one wave that waits until s_memrealtime reaches `deadline` (a delayed worker's sleep, ahead of
 // its task on its stream), at most `bound` ticks (then err bit 256)
 hipError_t launch_deadline(unsigned long long deadline, unsigned long long bound, unsigned* err, hipStream_t s);

@@ -772,6 +772,7 @@ def descent_kofn_dist(rank, world, port, config, epoch0, result_q):
               flush=True)
         if errors:
             errors.append(("median latency per worker (ms)", med_lat))
+            errors.append(("first epochs", [ln for ln in err.splitlines() if ln.startswith("[mpa descent]")][:12]))
         result_q.put(("ok", errors))
     except Exception:
         result_q.put(("exc", f"rank {rank}: " + traceback.format_exc()))
