@@ -31,19 +31,21 @@ namespace mpa {
 // polls instead -- 20 us asked, ~60 us of timer slack got -- moved the gated replays' median
 // harvest from 4 to 42 us and their worst from 1.0 to 1.5 ms: r05o.)
 constexpr int64_t kHotSpinNs = 50000;
+constexpr int64_t kServerHotSpinNs = 5000000;
 extern std::atomic<int64_t> g_timer_pending;  // host-timer launches pending in this process
 struct PoliteSpin {
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   uint32_t n = 0;
   bool cold = false;
   bool yield_cold = false;  // yield once cold whether or not a timer is pending
+  int64_t hot_ns = kHotSpinNs;
   void operator()() {
     if (cold && (yield_cold || g_timer_pending.load(std::memory_order_relaxed) > 0)) {
       std::this_thread::yield();
       return;
     }
     __builtin_ia32_pause();
-    if ((++n & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kHotSpinNs)) cold = true;
+    if ((++n & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(hot_ns)) cold = true;
   }
 };
 

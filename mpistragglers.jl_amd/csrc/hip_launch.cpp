@@ -30,9 +30,11 @@ struct QueueStream {
   hipStream_t s;
   int users;
   StreamKind kind;
+  bool reserved;  // its CU mask leaves the reserved CUs out
 };
 std::mutex g_stream_mu;
 std::vector<QueueStream> g_streams;
+std::atomic<int> g_past_cap{0};
 
 static int queue_cap() {
   static const int cap = [] {
@@ -53,14 +55,15 @@ void destroy_pooled_streams() {
   g_streams.clear();
 }
 
-hipStream_t make_queue_stream(int device, StreamKind kind) {
+hipStream_t make_queue_stream(int device, StreamKind kind, bool reserved) {
   static const bool registered = (std::atexit(destroy_pooled_streams), true);
   (void)registered;
+  reserved = reserved && kind != StreamKind::kCoord;
   std::lock_guard<std::mutex> lk(g_stream_mu);
   int have = 0;
   for (auto& q : g_streams)
     if (q.device == device) {
-      if (q.users == 0) {
+      if (q.users == 0 && q.reserved == reserved) {
         q.users = 1;
         q.kind = kind;
         return q.s;
@@ -70,22 +73,30 @@ hipStream_t make_queue_stream(int device, StreamKind kind) {
   if (have >= queue_cap()) {  // share the least-used one of the same kind
     QueueStream* best = nullptr;
     for (auto& q : g_streams)
-      if (q.device == device && q.kind == kind && (!best || q.users < best->users)) best = &q;
+      if (q.device == device && q.kind == kind && q.reserved == reserved && (!best || q.users < best->users)) best = &q;
     if (best) {
       best->users += 1;
       return best->s;
-    }  // none of this kind yet: one more queue past the cap
+    }
+    // none of this kind yet: one more queue past the cap, said once (the cap is
+    // no bound then; counter queues_past_cap)
+    if (g_past_cap++ == 0)
+      std::fprintf(stderr, "[mpa] %d CU-masked queues on device %d (MPA_MAX_QUEUES): one more for a stream kind "
+                   "that has none yet\n", have, device);
   }
   hipDeviceProp_t p;
   HIPCHECK(hipGetDeviceProperties(&p, device));
   const int cus = p.multiProcessorCount;
   std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0xFFFFFFFFu);
   if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+  if (reserved && cus >= 64) mask[0] &= ~((1u << kReservedCus) - 1u);  // CU 0 of each of the 8 XCDs
   hipStream_t s = nullptr;
   HIPCHECK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
-  g_streams.push_back({device, s, 1, kind});
+  g_streams.push_back({device, s, 1, kind, reserved});
   return s;
 }
+
+int queues_past_cap() { return g_past_cap.load(); }
 
 // The comm's own work is drained by its teardown (hipDeviceSynchronize in ~HipComm); a stream
 // another live comm still uses is not synchronised here, so releasing never blocks on that
@@ -251,7 +262,7 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
   };
   auto emit = [&]() {
     if (batch.empty()) return;
-    bs = (on_coord || coord_batches_) && !staged ? coord_ : pick_launch_stream();
+    bs = (on_coord || (coord_batches_ && !split_local_)) && !staged ? coord_ : pick_launch_stream();
     if (staged) stage_in(batch, bs);
     else if (bs != coord_) after_exchange(bs);
     if (batch_kind == MPA_TASK_LSQ_BATCH) launch_lsqb_batch(batch, bs);
@@ -704,8 +715,9 @@ HipComm::LsqbLaunch HipComm::build_lsqb_batch(const std::vector<int64_t>& ranks,
     b.pfd = lsqp_pfd_ >= 0 ? lsqp_pfd_ : (lsqp8_ ? 0 : 1);
     { const char* d = measure_env("MPA_LSQP_DBG"); b.dbg = d ? std::atoi(d) : 0; }
     // one workgroup per CU: 128 pairs (256 workgroups), dealt evenly over max(tasks,
-    // share) tasks
-    constexpr int target = 128;
+    // share) tasks; 120 (240) where the task streams leave one CU per XCD to the coordinator
+    // (reserve_cus_: 31 CUs per XCD, a pair's two members on one XCD)
+    const int target = reserve_cus_ ? 120 : 128;
     const int split = std::max(b.ntasks, share > 0 ? share : lsqb_share());
     int pairs = 0;
     for (int k = 0; k < b.ntasks; ++k) {

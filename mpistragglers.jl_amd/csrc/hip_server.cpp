@@ -15,8 +15,13 @@ void HipComm::serve() {
     ~Disarm() { c->disarm_all(); }
   } disarm_guard{this};
   std::vector<int64_t> fresh;
-  PoliteSpin idle;  // the doorbell poll between tasks (hot for kHotSpinNs, then yielding)
+  // the doorbell poll between tasks: hot for 5 ms after the last task (an epoch's gap between a
+  // worker's reply and its next doorbell), then yielding; with a 50 us window the serve loops of
+  // the one-GPU eight-process tests yielded their cores between epochs and saw doorbells
+  // milliseconds late on a loaded box (r06h)
+  PoliteSpin idle;
   idle.yield_cold = true;
+  idle.hot_ns = kServerHotSpinNs;
   for (int64_t r = 1; r <= nworkers_; ++r)
     if (w_[size_t(r - 1)].here && server_path(r) && armable(r)) arm(r);
   for (uint64_t spins = 0;; ++spins) {
@@ -91,12 +96,14 @@ void HipComm::serve() {
       launch_tasks(fresh, /*staged=*/true);
       idle = PoliteSpin{};
       idle.yield_cold = true;
+      idle.hot_ns = kServerHotSpinNs;
     } else if (!progress) {
       if ((spins & 0xFFF) == 0xFFF) watchdog(t0, /*timeout=*/false);
       idle();
     } else {
       idle = PoliteSpin{};  // busy again: the next idle stretch starts hot
       idle.yield_cold = true;
+      idle.hot_ns = kServerHotSpinNs;
     }
   }
 }

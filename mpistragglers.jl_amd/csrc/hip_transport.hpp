@@ -100,10 +100,14 @@ inline int lsqb_grid(int pass) {
 // cap (MPA_MAX_QUEUES) streams are shared.
 constexpr int kDefaultMaxQueues = 10;  // 12 until round 5; the comm's own coordinator stream is one of them
 enum class StreamKind { kWorker, kLaunch, kCoord };
-hipStream_t make_queue_stream(int device, StreamKind kind);
+// reserved: the stream leaves CU 0 of every XCD (CU-mask bits 0-7, tools/probe_cumask.hip:
+// bit b is CU b / 8 of XCD b % 8) to the coordinator's own stream (DESIGN.md §5, N > 1)
+hipStream_t make_queue_stream(int device, StreamKind kind, bool reserved = false);
+constexpr int kReservedCus = 8;
 void release_queue_stream(int device, hipStream_t s);
 bool stream_shared(hipStream_t s);  // more than one worker / comm launches on it
 int queue_streams(int device);      // CU-masked streams the process holds on the device
+int queues_past_cap();             // queues created past the cap (a stream kind that had none)
 
 struct HipWorker {
   bool here = true;     // its tasks run in this process
@@ -259,9 +263,20 @@ class HipComm final : public Comm {
   // epoch step, up to 5.7 ms per harvest; profiles/r05_null_stream.txt).  The comm's stream is
   // a blocking stream itself, so HIP still orders it with the caller's NULL-stream work both
   // ways.  MPA_OWN_COORD=0 keeps the NULL stream.
+  // The caller's stream (the Python layer passes torch's current one when it changes; Julia
+  // the task-local one).  The NULL stream becomes the comm's own blocking stream, which HIP
+  // still orders with the caller's NULL-stream work both ways.  A change of coordinator stream
+  // orders the new one after everything already queued on the old (a launch-ahead epoch, a
+  // pre-armed head): ADVICE r05.  Work the caller queues on OTHER streams is the caller's to
+  // order (torch: wait_stream on the current stream), as for any kernel library.
   void set_stream(hipStream_t s) {
     caller_null_ = s == nullptr || s == hipStreamLegacy;
-    coord_ = caller_null_ && own_coord_ ? own_coord_ : s;
+    hipStream_t next = caller_null_ && own_coord_ ? own_coord_ : s;
+    if (next != coord_) {
+      HIPCHECK(hipEventRecord(switch_ev_, coord_));
+      HIPCHECK(hipStreamWaitEvent(next, switch_ev_, 0));
+    }
+    coord_ = next;
   }
   hipStream_t stream() const { return coord_; }
 
@@ -588,12 +603,12 @@ class HipComm final : public Comm {
 
   // the worker's own stream (delayed tasks, pre-armed tasks), created on first use
   hipStream_t worker_stream(HipWorker& w) {
-    if (!w.stream) w.stream = make_queue_stream(dev_, StreamKind::kWorker);
+    if (!w.stream) w.stream = make_queue_stream(dev_, StreamKind::kWorker, reserve_cus_);
     return w.stream;
   }
   // launch stream k (created on first use, up to kLaunchStreams)
   hipStream_t launch_stream(size_t k) {
-    while (launch_streams_.size() <= k) launch_streams_.push_back(make_queue_stream(dev_, StreamKind::kLaunch));
+    while (launch_streams_.size() <= k) launch_streams_.push_back(make_queue_stream(dev_, StreamKind::kLaunch, reserve_cus_));
     return launch_streams_[k];
   }
 
@@ -781,6 +796,15 @@ class HipComm final : public Comm {
   // 19.9 vs 11.1 ms per epoch, profiles/r02_c5_lsqp_tuning.txt)
   bool lsqp_share_ = false;
   int here_count_ = 0;       // workers this process serves
+  // N > 1: on rank 0, tasks of a k-of-n call run on launch streams instead of
+  // behind the epoch step on the coordinator's stream (split_local_), so the next step never
+  // waits for rank 0's own straggler; and every task stream on rank 0's GPU -- rank 0's, and a
+  // worker process's that shares the GPU (the one-GPU rehearsal) -- leaves CU 0 of each XCD to
+  // the coordinator's stream (reserve_cus_), so the step finds a CU while a task holds the rest
+  // (lsqp4 fills every CU's register file: its grid shrinks to fit)
+  hipEvent_t switch_ev_ = nullptr;  // set_stream: the old coordinator stream's tail
+  bool split_local_ = false;
+  bool reserve_cus_ = false;
   bool hold_ok_ = true;     // MPA_HOLD=0: a stale re-dispatch launches at once (flush_stale)
   bool hold_next_ = false;  // set while flush_stale() flushes
   bool may_hold_ = false;   // this call's wait completes without the held tasks (set_wait_hold)

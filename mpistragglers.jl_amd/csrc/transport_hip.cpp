@@ -103,6 +103,13 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   int here_count = 0;
   for (const auto& w : w_) here_count += w.here;
   here_count_ = here_count;
+  bool any_remote = false, coord_gpu = false;
+  for (const auto& w : w_) {
+    any_remote |= w.remote;
+    if (role_ == SERVER && w.here && w.box) coord_gpu |= w.box->coord_dev == dev_;
+  }
+  split_local_ = role_ == COORD && any_remote && !env_off("MPA_SPLIT_LOCAL");
+  reserve_cus_ = ((role_ == COORD && any_remote) || (role_ == SERVER && coord_gpu)) && !env_off("MPA_RESERVE_CUS");
   const char* eager = measure_env("MPA_EAGER_STREAMS");
   if (eager && *eager == '1') {
     for (auto& w : w_)
@@ -114,6 +121,7 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   // the coordinator's own stream, in place of the NULL stream (set_stream)
   if (role_ != SERVER && !env_off("MPA_OWN_COORD")) coord_ = own_coord_ = make_queue_stream(dev_, StreamKind::kCoord);
   HIPCHECK(hipEventCreateWithFlags(&xfer_ev_, hipEventDisableTiming));
+  HIPCHECK(hipEventCreateWithFlags(&switch_ev_, hipEventDisableTiming));
   int khz = 0;
   HIPCHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
   rt_hz_ = khz > 0 ? double(khz) * 1e3 : 100e6;
@@ -227,6 +235,7 @@ HipComm::~HipComm() {
     (void)hipHostFree(pre_mb_);
   }
   if (xfer_ev_) (void)hipEventDestroy(xfer_ev_);
+  if (switch_ev_) (void)hipEventDestroy(switch_ev_);
   delete region_;
 }
 
@@ -851,6 +860,8 @@ int64_t HipComm::counter(const char* name) const {
   if (k == "clock_samples") return n_clock_samples_.load(std::memory_order_relaxed);  // host <-> device clock samples behind the deadlines
   if (k == "timer_late") return n_timer_late_.load(std::memory_order_relaxed);  // > 1 ms late timer launches
   if (k == "queues") return queue_streams(dev_);  // CU-masked streams (HSA queues) the process holds
+  if (k == "queues_past_cap") return queues_past_cap();
+  if (k == "reserved_cus") return reserve_cus_ ? kReservedCus : 0;  // CUs this process's task streams leave out
   if (k == "shared_worker_streams") {  // workers whose stream another worker or comm also uses
     int64_t k2 = 0;
     for (const auto& w : w_)

@@ -186,6 +186,43 @@ def test_queue_cap(M, torch_mod):
     c.close()
 
 
+_PAST_CAP_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import torch
+import mpiasyncpools as M
+c = M.DeviceComm(2)          # its coordinator stream takes the one queue MPA_MAX_QUEUES=1 allows
+for r in (1, 2):
+    c.set_task(r, "kmap2")   # worker 1: a kind with no stream yet -> one queue past the cap
+pool = M.MPIAsyncPool(2)     # worker 2: shares worker 1's
+rb = torch.zeros(6, dtype=torch.float64, device="cuda")
+M.asyncmap_(pool, torch.ones(1, dtype=torch.float64, device="cuda"), rb, torch.zeros(2, dtype=torch.float64, device="cuda"),
+            torch.zeros_like(rb), c, nwait=2)
+print("RESULT", c.counter("queues"), c.counter("queues_past_cap"), c.counter("shared_worker_streams"),
+      rb.cpu().numpy().reshape(2, 3)[:, 0].tolist())
+c.close()
+"""
+
+
+def test_queue_past_cap_is_counted_and_said(M):
+    """past MPA_MAX_QUEUES a stream kind that has no stream yet still gets a queue
+    (a coordinator or worker stream cannot share another kind's), but no longer silently: the
+    process says so once on stderr and counts it (counter queues_past_cap).  The cap is read once
+    per process: a child with MPA_MAX_QUEUES=1."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpistragglers.jl_amd")
+    r = subprocess.run([sys.executable, "-c", _PAST_CAP_CHILD, pkg], env=dict(os.environ, MPA_MAX_QUEUES="1"),
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][-1].split(maxsplit=4)
+    queues, past, shared = int(line[1]), int(line[2]), int(line[3])
+    assert (queues, past, shared) == (2, 1, 2), line
+    assert line[4] == "[1.0, 2.0]", line
+    assert "one more for a stream kind that has none yet" in r.stderr
+
+
 def test_device_delays_only_on_unshared_streams(M, torch_mod, monkeypatch):
     """MPA_DELAY=device (forced; by default only where no caller work on the NULL stream can meet
     it): a delayed task waits behind a one-wave deadline kernel ahead of it on its worker's
