@@ -798,10 +798,11 @@ class HipComm final : public Comm {
   int here_count_ = 0;       // workers this process serves
   // N > 1: on rank 0, tasks of a k-of-n call run on launch streams instead of
   // behind the epoch step on the coordinator's stream (split_local_), so the next step never
-  // waits for rank 0's own straggler; and every task stream on rank 0's GPU -- rank 0's, and a
-  // worker process's that shares the GPU (the one-GPU rehearsal) -- leaves CU 0 of each XCD to
-  // the coordinator's stream (reserve_cus_), so the step finds a CU while a task holds the rest
-  // (lsqp4 fills every CU's register file: its grid shrinks to fit)
+  // waits for rank 0's own straggler (MPA_SPLIT_LOCAL=0: as before); and, opt-in
+  // (MPA_RESERVE_CUS=1), every task stream on rank 0's GPU -- rank 0's, and a worker process's
+  // that shares the GPU (the one-GPU rehearsal) -- leaves CU 0 of each XCD to the coordinator's
+  // stream (reserve_cus_), so the step finds a CU while a task holds the rest (lsqp4 fills every
+  // CU's register file: its grid shrinks to fit)
   hipEvent_t switch_ev_ = nullptr;  // set_stream: the old coordinator stream's tail
   bool split_local_ = false;
   bool reserve_cus_ = false;

@@ -109,7 +109,11 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
     if (role_ == SERVER && w.here && w.box) coord_gpu |= w.box->coord_dev == dev_;
   }
   split_local_ = role_ == COORD && any_remote && !env_off("MPA_SPLIT_LOCAL");
-  reserve_cus_ = ((role_ == COORD && any_remote) || (role_ == SERVER && coord_gpu)) && !env_off("MPA_RESERVE_CUS");
+  // (opt-in, MPA_RESERVE_CUS=1: on the one-GPU rehearsal the reserved CUs cost c5 at N = 2 a
+  // third of its rate -- 84 against 128 it/s, r06k -- while the split alone already brought the
+  // epoch step from 236-356 us to 16 us; on the node it is unmeasured)
+  const char* rc = std::getenv("MPA_RESERVE_CUS");
+  reserve_cus_ = ((role_ == COORD && any_remote) || (role_ == SERVER && coord_gpu)) && rc && *rc == '1';
   const char* eager = measure_env("MPA_EAGER_STREAMS");
   if (eager && *eager == '1') {
     for (auto& w : w_)

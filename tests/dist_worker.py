@@ -552,7 +552,7 @@ def lsq_sched_dist(rank, world, port, placement, config, epoch0, result_q):
 # lives on rank 0 and is made the straggler -- c3 by an injected 10 ms delay per task, c5 by a shard
 # 4096x the others' (an undelayed task: the kind a stale re-dispatch may hold) -- so its stale
 # replies and re-dispatches (src/MPIAsyncPools.jl:177-184) happen every few epochs; remote workers
-# carry injected delays (`remote`: Exp(mean ms) per task, or "spikes": 3 ms every 4th task of the
+# carry injected delays (`remote`: Exp(mean ms) per task, or "spikes": 20 ms every 4th task of the
 # last worker, none for the others), their stale replies harvested from other processes' GPUs.
 # eta keeps the slow worker's gradient from converging towards zero over the run (its own L =
 # rows / (3 cols) is large): a gradient that cancels down to its rounding has no relative accuracy
@@ -568,7 +568,7 @@ KOFN_CONFIGS = {
     # c5: the batched 64-iterate variant (bf16 messages, fp32 accumulate), nwait 7 of 8; rank 0
     # serves workers 1 (slow: ~1 ms of lsqp4) and 2 (fast); worker 2's next task queues behind
     # worker 1's running launch on the coordinator stream, so worker 1's stale re-dispatch is
-    # HELD and joins worker 2's next launch; the last worker's 3 ms spikes make it the stale one
+    # HELD and joins worker 2's next launch; the last worker's 20 ms spikes make it the stale one
     # now and then
     "c5": dict(dt="bf16", cols=2048, nwait=7, stale=0.0, tol=1e-5, placement=[0, 0, 1, 2, 3, 4, 5, 6],
                rows=[1 << 20] + [256] * 7, local_delay_ms=None, remote="spikes", epochs=30, eta=2e-5, k=64),
@@ -632,7 +632,7 @@ def descent_kofn_dist(rank, world, port, config, epoch0, result_q):
                 comm.set_delays(w, [int(cfg["local_delay_ms"] * 1e6)])
             elif rank != 0 and cfg["remote"] == "spikes":
                 if w == n:
-                    comm.set_delays(w, [0, 0, 0, 3_000_000])
+                    comm.set_delays(w, [0, 0, 0, 20_000_000])
             elif rank != 0:
                 rng = np.random.default_rng([17, w])
                 comm.set_delays(w, rng.exponential(cfg["remote"] * 1e6, size=512).astype(np.int64))
