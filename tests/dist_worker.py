@@ -549,7 +549,7 @@ def lsq_sched_dist(rank, world, port, placement, config, epoch0, result_q):
 
 # The native k-of-n loop across processes: what bench.py's rank 0 runs at
 # N > 1 for c3 / c4 / c5 (make_loop: mpa_lsq_descent / mpa_lsqb_descent on a DistComm).  Worker 1
-# lives on rank 0 and is made the straggler -- c3 by an injected 10 ms delay per task, c5 by a shard
+# lives on rank 0 and is made the straggler -- c3 by an injected 30 ms delay per task, c5 by a shard
 # 4096x the others' (an undelayed task: the kind a stale re-dispatch may hold) -- so its stale
 # replies and re-dispatches (src/MPIAsyncPools.jl:177-184) happen every few epochs; remote workers
 # carry injected delays (`remote`: Exp(mean ms) per task, or "spikes": 20 ms every 4th task of the
@@ -561,7 +561,7 @@ KOFN_CONFIGS = {
     # c3: fp32, nwait 6 of 8, stale results dropped; the node's placement (rank 0 serves worker
     # 1 only), so worker 1's stale re-dispatch launches at once (nothing else of rank 0's runs)
     "c3": dict(dt="f32", cols=2048, nwait=6, stale=0.0, tol=1e-5, placement=list(range(8)),
-               rows=[256] * 8, local_delay_ms=10.0, remote=0.1, epochs=40, eta=0.05),
+               rows=[256] * 8, local_delay_ms=30.0, remote=0.1, epochs=60, eta=0.05),
     # c4: fp64, worker 1 fresh + 5 others (first_plus), stale results at weight 0.5; worker 1 fast
     "c4": dict(dt="f64", cols=2048, nwait="first_plus5", stale=0.5, tol=1e-12, placement=list(range(8)),
                rows=[256] * 8, local_delay_ms=None, remote=1.0, epochs=40, eta=0.05),
@@ -756,9 +756,13 @@ def descent_kofn_dist(rank, world, port, config, epoch0, result_q):
             e_i = float(torch.linalg.norm(ch[i] - g) / torch.linalg.norm(g))
             if not e_i <= tol:
                 errors.append(("final chunk", i, r, e_i))
-        if not stale_remote >= 1:
+        # the stale paths the node's run takes (their mix depends on the box's timing: remote
+        # workers of eight processes on one loaded GPU range from 0.1 to 10 ms, r06l)
+        if config == "c4" and not stale_remote >= 1:
             errors.append(("no remote stale harvest", stale_remote))
-        if config in ("c3", "c5") and not stale_local >= 1:
+        if config == "c3" and not stale_local + stale_remote >= 1:
+            errors.append(("no stale harvest", stale_local, stale_remote))
+        if config == "c5" and not stale_local >= 1:
             errors.append(("no stale harvest of the slow local worker", stale_local))
         if config == "c3" and got["held"] != 0:
             errors.append(("held a re-dispatch with nothing else of rank 0's in flight", got))
