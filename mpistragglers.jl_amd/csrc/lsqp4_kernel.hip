@@ -97,7 +97,8 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 }
 // MPA_LSQP4_PROBE (timing-probe builds only, wrong results: make BUILD=... EXTRA=-DMPA_LSQP4_PROBE=n,
 // profiles/r03_c5_probes.txt): 1 no strip DMAs in the block loop, 2 no cross-wave exchange /
-// barrier in the reduce, 4 no phase-1 MFMAs, 8 half the phase-2 LDS reads (r04_c5_pipelined.txt)
+// barrier in the reduce, 4 no phase-1 MFMAs, 8 half the phase-2 LDS reads (r04_c5_pipelined.txt),
+// 16 no L2 prefetch (r06: 1 | 16 = the loop with no memory traffic but B, profiles/r06_c5_prefetch_cu.txt)
 #ifndef MPA_LSQP4_PROBE
 #define MPA_LSQP4_PROBE 0
 #endif
@@ -638,7 +639,9 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
       dma_strip(nb2, vf, vp, c, slot);
 #endif
     }
+#if !(MPA_LSQP4_PROBE & 16)  // timing probe 16: no L2 prefetch in the loop
     pf(kb0 + u + 2 + pfd);
+#endif
   };
 #if MPA_MEASURE
   unsigned long long clk0 = 0, rt0 = 0;
