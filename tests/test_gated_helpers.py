@@ -97,3 +97,54 @@ def test_hop_check_on_the_oracles_own_timeline():
     slow[5, gated.F["harvest"]] += 2_000_000  # one harvest 2 ms after its trigger
     kinds = {b[0] for b in gated.hop_check(sc, got, slow)[0]}
     assert "harvest" in kinds and "latency" in kinds
+
+
+def test_hop_check_harvest_held_back_by_the_previous_harvest():
+    """A harvest cannot precede the call's previous harvest (the state machine harvests one
+    completion at a time, in the oracle's order): when the chain drift posts a task late -- on time
+    against its own post, so its task hop holds -- the next harvest of the same call waits for it,
+    and that is not the next harvest's lateness (kmap2_n9 op 356, r06g).  A harvest late past its
+    trigger AND the previous harvest is still a miss."""
+    import numpy as np
+    sc = next(s for s in gated.scenarios() if s["name"] == "kmap2_n9")
+    got, tr = _synthetic(sc)
+    F = gated.F
+    starts = np.asarray([g["t_ns"][0] for g in got], dtype=np.int64)
+    calls = np.searchsorted(starts, tr[:, F["harvest"]], side="right") - 1
+    # a call with two harvests at different instants (a, then b)
+    pair = None
+    for k in np.unique(calls):
+        idx = sorted(np.nonzero(calls == k)[0], key=lambda j: tr[j, F["harvest"]])
+        end = starts[k + 1] if k + 1 < len(starts) else np.iinfo(np.int64).max
+        for a, b in zip(idx, idx[1:]):
+            room = end - tr[b, F["harvest"]] - (tr[b, F["pub"]] - tr[a, F["harvest"]])
+            if tr[a, F["harvest"]] < tr[b, F["harvest"]] and tr[a, F["rank"]] != tr[b, F["rank"]] and room > 3_000_000:
+                pair = (int(k), a, b)
+                break
+        if pair:
+            break
+    assert pair, "no call with two consecutive harvests"
+    k, a, b = pair
+    ranks = got[k]["ranks"]
+    ia, ib = ranks.index(int(tr[a, F["rank"]])), ranks.index(int(tr[b, F["rank"]]))
+    # task a posted late by the chain (on time against that post), so late that b -- which completed
+    # after a on the oracle's clock -- completes before a now
+    drift = int(tr[b, F["pub"]] - tr[a, F["harvest"]]) + 500_000
+    held = tr.copy()
+    for key in ("post", "due", "pub", "seen", "harvest"):
+        held[a, F[key]] += drift
+    new_b = held[a, F["harvest"]] + 1_000  # b harvested right after a
+    lat = [list(g["latency_s"]) for g in got]
+    lat[k][ib] += (new_b - held[b, F["harvest"]]) / 1e9
+    held[b, F["seen"]] = held[b, F["harvest"]] = new_b
+    got2 = [dict(g, latency_s=lat[j]) for j, g in enumerate(got)]
+    bad = gated.hop_check(sc, got2, held)[0]
+    assert bad == [], bad[:3]
+    # b 2 ms after a's harvest as well: late past both its trigger and the previous harvest
+    later = held.copy()
+    later[b, F["seen"]] = later[b, F["harvest"]] = new_b + 2_000_000
+    lat[k][ib] += 2e-3
+    got3 = [dict(g, latency_s=lat[j]) for j, g in enumerate(got)]
+    kinds = {(x[0], x[1], x[2]) for x in gated.hop_check(sc, got3, later)[0]}
+    assert ("harvest", k, ib) in kinds, kinds
+    del ia
