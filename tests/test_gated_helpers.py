@@ -129,7 +129,7 @@ def test_hop_check_harvest_held_back_by_the_previous_harvest():
     ia, ib = ranks.index(int(tr[a, F["rank"]])), ranks.index(int(tr[b, F["rank"]]))
     # task a posted late by the chain (on time against that post), so late that b -- which completed
     # after a on the oracle's clock -- completes before a now
-    drift = int(tr[b, F["pub"]] - tr[a, F["harvest"]]) + 500_000
+    drift = int(tr[b, F["pub"]] - tr[a, F["harvest"]]) + 1_500_000
     held = tr.copy()
     for key in ("post", "due", "pub", "seen", "harvest"):
         held[a, F[key]] += drift
