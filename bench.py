@@ -383,7 +383,7 @@ def report(args, cfg, world, el, per_rank, extra):
 
 ROCPROF_STATS = {"c2": ("%s_c2_kernel_stats.csv", "lsq_grad_kernel"),
                  "c5": ("%s_c5_kernel_stats.csv", "lsqp4_kernel")}
-PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")   # newest first
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03", "r02")   # newest first
 
 
 def rocprof_avg_ms(cfg):
