@@ -52,6 +52,13 @@ __device__ __forceinline__ void publish_done_local(unsigned long long* flag, uns
 __device__ __forceinline__ void publish_done_wt(unsigned long long* flag, unsigned long long seq) {
   __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// N > 1: a worker process's task also stores its completion into rank 0's GPU memory (a word
+// after its reply inbox, over xGMI), where rank 0's fused tail / wait kernel polls it instead of
+// the host-memory word across PCIe (round 6).  After publish_done's system-scope fence: the reply
+// is visible before either word.
+__device__ __forceinline__ void publish_peer(unsigned long long* flag2, unsigned long long seq) {
+  if (flag2) __hip_atomic_store(flag2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void publish_task(unsigned long long* flag, unsigned long long seq, int local) {
   if (local) publish_done_local(flag, seq);
   else publish_done(flag, seq);

@@ -586,6 +586,7 @@ LsqBatch HipComm::build_lsq_batch(const std::vector<int64_t>& ranks, int dtype, 
     t.slab = w.slab;
     t.ctr = ctr_ + kLsqCtrPerTask * (rank - 1);
     t.flag = w.flag_dev;
+    t.flag2 = peer_done(w);
     t.seq = w.seq;
     t.rows = ts.rows;
     t.lda = ts.lda;
@@ -732,6 +733,7 @@ HipComm::LsqbLaunch HipComm::build_lsqb_batch(const std::vector<int64_t>& ranks,
       t.slab = w.lsqp_slab;
       t.ctr = w.lsqp_ctr;
       t.flag = w.flag_dev;
+      t.flag2 = peer_done(w);
       t.seq = w.seq;
       t.rows = ts.rows;
       t.lda = ts.lda;
@@ -851,6 +853,7 @@ HipComm::LsqbLaunch HipComm::build_lsqb_batch(const std::vector<int64_t>& ranks,
     t.slab = w.lsqb_slab;
     t.ctr = w.lsqb_ctr;
     t.flag = w.flag_dev;
+    t.flag2 = peer_done(w);
     t.seq = w.seq;
     t.rows = ts.rows;
     t.lda = ts.lda;

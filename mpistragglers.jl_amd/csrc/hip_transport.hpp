@@ -804,6 +804,23 @@ class HipComm final : public Comm {
   // stream (reserve_cus_), so the step finds a CU while a task holds the rest (lsqp4 fills every
   // CU's register file: its grid shrinks to fit)
   hipEvent_t switch_ev_ = nullptr;  // set_stream: the old coordinator stream's tail
+  // N > 1, device payload path: each remote worker's completion word has a device copy after
+  // its reply inbox in rank 0's memory (publish_peer), which rank 0's kernels poll instead of
+  // the host-memory word (MPA_DONE_DEV=0: the host word only, as before round 6)
+  bool done_dev_ = true;
+  size_t done_off() const { return region_ ? (region_->max_msg() + 255) / 256 * 256 : 0; }
+  // the server's task: rank 0's device done word of worker w (mapped by IPC), or null
+  unsigned long long* peer_done(const HipWorker& w) const {
+    return role_ == SERVER && done_dev_ && w.path_dev && w.peer_reply
+               ? reinterpret_cast<unsigned long long*>(w.peer_reply + done_off())
+               : nullptr;
+  }
+  // rank 0: the word its kernels poll for remote worker w's completion
+  const unsigned long long* remote_done_word(const HipWorker& w) const {
+    return done_dev_ && w.path_dev && w.reply_inbox
+               ? reinterpret_cast<const unsigned long long*>(w.reply_inbox + done_off())
+               : region_->dev(&w.box->done);
+  }
   bool split_local_ = false;
   bool reserve_cus_ = false;
   bool hold_ok_ = true;     // MPA_HOLD=0: a stale re-dispatch launches at once (flush_stale)

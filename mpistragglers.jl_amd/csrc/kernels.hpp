@@ -104,6 +104,7 @@ struct LsqTask {
   void* slab;       // [grid][cols_pad] partial sums (T), reduced in place
   uint32_t* ctr;    // [kLsqCtrPerTask] reduction-tree arrival counters, zero between launches
   unsigned long long* flag;  // host-pinned completion word of the worker
+  unsigned long long* flag2;  // N > 1, a worker process's task: rank 0's device copy of the done word, or null
   unsigned long long seq;
   int64_t rows, lda;
   int cols, grid;
@@ -228,6 +229,7 @@ struct LsqbTask {
   void* slab;   // [nrange][nslice][64 x 256] fp32 partials of pass 2
   uint32_t* ctr;  // [kLsqbMaxSlices] per-slice arrivals + [1] per-task slice completions
   unsigned long long* flag;
+  unsigned long long* flag2;  // N > 1, a worker process's task: rank 0's device copy of the done word, or null
   unsigned long long seq;
   int64_t rows, lda;
   int cols;
@@ -265,6 +267,7 @@ struct LsqpTask {
   uint32_t* ctr;   // [2 halves][8 waves][kLsqpCtrPerSlice] tree counters + [1] slice completions;
                    // every counter is reset by its last arriver
   unsigned long long* flag;
+  unsigned long long* flag2;  // N > 1, a worker process's task: rank 0's device copy of the done word, or null
   unsigned long long seq;
   int64_t rows, lda;
   int cols;

@@ -547,6 +547,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     if constexpr ((MODE & M_HEAD) != 0) MPA_HEAD_STAMP(batch.head_token, 4, false);
     if (a.pub_local) publish_done_wt(a.flag, a.seq);
     else publish_done(a.flag, a.seq);
+    publish_peer(a.flag2, a.seq);
   }
   if (!batch.tail) return;
   // Fused tail: this workgroup finished its task (and published it); the last task of the

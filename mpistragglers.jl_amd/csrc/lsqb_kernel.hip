@@ -548,7 +548,10 @@ __global__ void __launch_bounds__(kThreads, 2) lsqb_grad_kernel(LsqbBatch batch)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     drain_vm();
     const unsigned old = __hip_atomic_fetch_add(&a.ctr[kLsqbMaxSlices], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old - a.tbase == unsigned(nslice - 1)) publish_done(a.flag, a.seq);
+    if (old - a.tbase == unsigned(nslice - 1)) {
+      publish_done(a.flag, a.seq);
+      publish_peer(a.flag2, a.seq);
+    }
   }
 }
 

@@ -756,7 +756,10 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
                                                 __HIP_MEMORY_SCOPE_AGENT);
     if (old + 1 == unsigned(2 * QW)) {
       __hip_atomic_store(&a.ctr[2 * 8 * kLsqpCtrPerSlice], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (!cx) publish_task(a.flag, a.seq, a.pub_local);  // every slice read the same go word
+      if (!cx) {  // every slice read the same go word
+        publish_task(a.flag, a.seq, a.pub_local);
+        publish_peer(a.flag2, a.seq);
+      }
     }
   }
 }

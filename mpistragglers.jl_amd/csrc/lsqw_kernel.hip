@@ -222,6 +222,7 @@ __global__ void __launch_bounds__(kThreads) lsqw_grad_kernel(LsqBatch batch) {
     if (old + 1 == unsigned(nslice)) {
       __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       publish_done(a.flag, a.seq);
+      publish_peer(a.flag2, a.seq);
     }
   }
 }

@@ -58,6 +58,7 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
                          hipHostMallocCoherent | hipHostMallocMapped));
   std::memset(cancel_, 0, sizeof(unsigned long long) * size_t(n + 1));
   xgmi_ = !env_off("MPA_XGMI");
+  done_dev_ = !env_off("MPA_DONE_DEV");
   // per-task tree counters, then the doorbell ticket and the fused-tail counter
   HIPCHECK(hipMalloc(&ctr_, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 3)));
   HIPCHECK(hipMemset(ctr_, 0, sizeof(uint32_t) * (kLsqCtrPerTask * size_t(n) + 3)));
@@ -87,7 +88,9 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
     } else if (w.remote) {
       w.flag_host = &w.box->done;
       w.box->coord_dev = dev_;
-      w.reply_inbox = static_cast<uint8_t*>(ipc_alloc(region_->max_msg(), w.box->reply_handle, &w.box->reply_ipc));
+      // the reply inbox, then the device copy of the worker's completion word (publish_peer)
+      w.reply_inbox = static_cast<uint8_t*>(ipc_alloc(done_off() + 256, w.box->reply_handle, &w.box->reply_ipc));
+      HIPCHECK(hipMemset(w.reply_inbox + done_off(), 0, 256));
     } else {
       w.flag_host = &flags_[r - 1];
       w.flag_dev = &flags_[r - 1];
@@ -800,7 +803,7 @@ void HipComm::maybe_ahead() {
           HIPCHECK(launch_wait_words(ww, coord_));
           ww.n = 0;
         }
-        ww.word[ww.n] = region_->dev(&w.box->done);
+        ww.word[ww.n] = remote_done_word(w);
         ww.target[ww.n] = w.seq;
         ++ww.n;
       }
@@ -827,7 +830,7 @@ void HipComm::maybe_ahead() {
         ++tail_ranks_;
         continue;
       }
-      tail_word_[tail_nwait_] = region_->dev(&w.box->done);
+      tail_word_[tail_nwait_] = remote_done_word(w);
       tail_target_[tail_nwait_++] = w.seq;
     }
     tail_next_ = true;
