@@ -368,6 +368,7 @@ void lsqf_prof_dump();  // MPA_LSQF_DBG & 16: wait-cycle breakdown to stderr
 void head_stamp_reset();  // MPA_HEAD_STAMP=1 (measurement build): the fused-head launch stamps
 void head_stamp_dump();
 void lsqp4_clock_dump();  // MPA_LSQP4_CLOCK=1: lsqp4's in-kernel clock of its last launch to stderr
+void lsq_stamp_dump();    // MPA_LSQ_STAMP=1: lsq_grad_kernel's last launch timeline to stderr
 
 struct KmapArgs {
   int kind;

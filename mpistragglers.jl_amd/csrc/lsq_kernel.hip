@@ -162,8 +162,21 @@ __device__ __forceinline__ void head_stamp(uint32_t token, int k, bool first) {
   else atomicMax(p, rt_now());
 }
 #define MPA_HEAD_STAMP(tok, k, first) head_stamp(tok, k, first)
+// measurement build (MPA_LSQ_STAMP=1 dumps them): s_memrealtime of the last launch, per workgroup
+// [0] entry and [1] end of its block loop; the launch's last tree root start and last publish
+constexpr int kLsqStampWgs = 1024;
+__device__ unsigned long long g_lsq_wg[kLsqStampWgs][2];
+__device__ unsigned long long g_lsq_root, g_lsq_pub;
+__device__ unsigned g_lsq_grid;
+#define MPA_LSQ_WG_STAMP(k) \
+  do {                     \
+    if (threadIdx.x == 0 && blockIdx.x < kLsqStampWgs) g_lsq_wg[blockIdx.x][k] = rt_now(); \
+  } while (0)
+#define MPA_LSQ_MAX_STAMP(v) atomicMax(&(v), rt_now())
 #else
 #define MPA_HEAD_STAMP(tok, k, first) (void)0
+#define MPA_LSQ_WG_STAMP(k) (void)0
+#define MPA_LSQ_MAX_STAMP(v) (void)0
 #endif
 
 template <typename T, int VPL, int RB, int MODE>
@@ -181,6 +194,10 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   const int blk = int(blockIdx.x) - batch.block0[ti];
   if constexpr ((MODE & M_ARMED) != 0)
     if (!wait_door(a.door, a.seq, batch.spin_ticks, batch.err)) return;  // device-armed
+  MPA_LSQ_WG_STAMP(0);
+#if MPA_MEASURE
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_lsq_grid = gridDim.x;
+#endif
   // A pre-armed task its server cancelled (the host-memory go word holds its seq) computes
   // but neither writes its reply nor publishes.  The word is read ONCE, by the workgroup that
   // writes the reply, at that point: every lane of every workgroup reading it before any work
@@ -379,6 +396,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     }
   }
 
+  MPA_LSQ_WG_STAMP(1);
   // workgroup partial, waves added in fixed order
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) {
@@ -514,6 +532,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       if (!s_ticket) return;  // an earlier arriver of the group: the last one carries it
       const unsigned next = (count + F - 1) / F;
       if (next == 1) cx = cancelled();
+      if (next == 1 && tid == 0) MPA_LSQ_MAX_STAMP(g_lsq_root);
       const P* src = slab + size_t(first) * stride * S;
       for (int j = tid; j < S; j += kThreads) {
         P t[F];
@@ -548,6 +567,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     if (a.pub_local) publish_done_wt(a.flag, a.seq);
     else publish_done(a.flag, a.seq);
     publish_peer(a.flag2, a.seq);
+    MPA_LSQ_MAX_STAMP(g_lsq_pub);
   }
   if (!batch.tail) return;
   // Fused tail: this workgroup finished its task (and published it); the last task of the
@@ -729,6 +749,36 @@ static int v2048() {
 #endif
 
 const char* lsq_variant_name() { return kC2Variants[c2_variant()].name; }
+
+#if MPA_MEASURE
+// MPA_LSQ_STAMP=1 (measurement build): the last lsq_grad_kernel launch's timeline, from its first
+// workgroup's entry (us): the last entry, the block loops' ends (median, last), the last tree
+// root's start and the last publish
+void lsq_stamp_dump() {
+  static unsigned long long wg[kLsqStampWgs][2];
+  unsigned long long root = 0, pub = 0;
+  unsigned grid = 0;
+  if (hipMemcpyFromSymbol(wg, HIP_SYMBOL(g_lsq_wg), sizeof(wg)) != hipSuccess ||
+      hipMemcpyFromSymbol(&root, HIP_SYMBOL(g_lsq_root), sizeof(root)) != hipSuccess ||
+      hipMemcpyFromSymbol(&pub, HIP_SYMBOL(g_lsq_pub), sizeof(pub)) != hipSuccess ||
+      hipMemcpyFromSymbol(&grid, HIP_SYMBOL(g_lsq_grid), sizeof(grid)) != hipSuccess)
+    return;
+  const unsigned n = grid < unsigned(kLsqStampWgs) ? grid : unsigned(kLsqStampWgs);
+  if (!n) return;
+  unsigned long long t0 = ~0ull, s1 = 0;
+  std::vector<double> ends;
+  for (unsigned b = 0; b < n; ++b) {
+    t0 = std::min(t0, wg[b][0]);
+    s1 = std::max(s1, wg[b][0]);
+  }
+  for (unsigned b = 0; b < n; ++b) ends.push_back(double(wg[b][1] - t0) / 100.0);
+  std::sort(ends.begin(), ends.end());
+  std::fprintf(stderr, "[mpa lsq stamps] last launch, %u workgroups (us from the first entry): last entry %.2f, "
+               "loop ends p10 %.2f median %.2f last %.2f, last tree root %.2f, last publish %.2f\n", n,
+               double(s1 - t0) / 100.0, ends[n / 10], ends[n / 2], ends.back(), double(root - t0) / 100.0,
+               double(pub - t0) / 100.0);
+}
+#endif
 
 #if MPA_MEASURE
 void head_stamp_reset() {

@@ -200,6 +200,7 @@ HipComm::~HipComm() {
 #if MPA_MEASURE
   if (const char* d = measure_env("MPA_LSQF_DBG"); d && (std::atoi(d) & 16)) lsqf_prof_dump();
   if (const char* d = measure_env("MPA_LSQP4_CLOCK"); d && *d == '1') lsqp4_clock_dump();
+  if (const char* d = measure_env("MPA_LSQ_STAMP"); d && *d == '1') lsq_stamp_dump();
   if (const char* d = measure_env("MPA_HEAD_STAMP"); d && *d == '1') head_stamp_dump();
 #endif
   for (auto& w : w_) {
