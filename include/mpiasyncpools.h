@@ -206,9 +206,13 @@ int mpa_comm_set_gate(mpa_comm* comm, int64_t nsteps, const int* kinds, const in
  * launches released with the step they predicted (no mailbox read), "stale_deferred" held
  * re-dispatches whose copies joined the next epoch step, "task_launches"
  * least-squares task launches, "armed" (worker process) tasks launched device-armed,
- * "sleeps" delayed tasks that slept on the device (MPA_DELAY=device), "timer_late" delayed
- * launches the host timer issued more than 1 ms after they were due, "queues" CU-masked streams (HSA queues) the process holds on the comm's device,
- * "shared_worker_streams" workers whose stream is shared past the queue cap. */
+ * "sleeps" delayed tasks that slept on the device (behind a deadline kernel, or in a worker
+ * process's doorbell wait), "clock_samples" host <-> device clock samples behind the deadlines,
+ * "timer_late" delayed launches the host timer issued more than 1 ms after they were due,
+ * "queues" CU-masked streams (HSA queues) the process holds on the comm's device,
+ * "queues_past_cap" queues created past the cap (a stream kind that had none),
+ * "shared_worker_streams" workers whose stream is shared past the queue cap, "reserved_cus"
+ * CUs this process's task streams leave to the coordinator (MPA_RESERVE_CUS=1). */
 int64_t mpa_comm_counter(mpa_comm* comm, const char* name);
 /* ---- multi-process communicators: one process per GPU ------- */
 /* placement[w] = the process rank that serves worker w+1 (rank 0 is the coordinator's own

@@ -92,7 +92,8 @@ class _Comm:
         """An event counter of the transport (mpa_comm_counter, include/mpiasyncpools.h):
         "held", "held_joined", "held_alone", "gate_steps", "head_steps", "epoch_kernels",
         "prearmed", "prearm_cancelled", "prearm_same", "stale_deferred", "task_launches",
-        "armed", "sleeps", "timer_late", "queues", "shared_worker_streams"; -1 if the transport does not count it."""
+        "armed", "sleeps", "clock_samples", "timer_late", "queues", "queues_past_cap",
+        "shared_worker_streams", "reserved_cus"; -1 if the transport does not count it."""
         return int(lib().mpa_comm_counter(self._h, name.encode()))
 
     def set_gate(self, kinds, offsets, ranks):
