@@ -262,7 +262,9 @@ void HipComm::launch_tasks(const std::vector<int64_t>& ranks, bool staged, bool 
   };
   auto emit = [&]() {
     if (batch.empty()) return;
+    MPA_HSTAMP('p', batch.front(), 0);
     bs = (on_coord || (coord_batches_ && !split_local_)) && !staged ? coord_ : pick_launch_stream();
+    MPA_HSTAMP('q', batch.front(), 0);
     if (staged) stage_in(batch, bs);
     else if (bs != coord_) after_exchange(bs);
     if (batch_kind == MPA_TASK_LSQ_BATCH) launch_lsqb_batch(batch, bs);
@@ -939,7 +941,9 @@ void HipComm::enqueue_lsq(const LsqBatch& b, int dtype, int cols, hipStream_t s,
   }
   {
     MPA_HPROF(kHpLaunch);
+    MPA_HSTAMP('k', armed_rank, timed);
     HIPCHECK(launch_lsq(dtype, cols, b, s));
+    MPA_HSTAMP('K', armed_rank, timed);
   }
   if (debug_) {
     const hipError_t e = hipStreamSynchronize(s);

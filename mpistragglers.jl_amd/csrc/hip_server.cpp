@@ -23,7 +23,7 @@ void HipComm::serve() {
   idle.yield_cold = true;
   idle.hot_ns = kServerHotSpinNs;
   for (int64_t r = 1; r <= nworkers_; ++r)
-    if (w_[size_t(r - 1)].here && server_path(r) && armable(r)) arm(r);
+    if (w_[size_t(r - 1)].here && server_path(r) && armable(r)) arm_up(r);
   for (uint64_t spins = 0;; ++spins) {
     if (__atomic_load_n(&h->shutdown, __ATOMIC_ACQUIRE) || __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE) != gen0) break;
     fresh.clear();
@@ -34,21 +34,25 @@ void HipComm::serve() {
       if (!w.path_known) {
         if (server_path(r)) {
           progress = true;
-          if (armable(r)) arm(r);
+          if (armable(r)) arm_up(r);
         }
         continue;
       }
       if (w.armed) {
-        if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) continue;
-        // the armed task ran: check what rank 0 posted against what it was armed for
-        w.armed = false;
+        // the oldest armed task ran: check what rank 0 posted against what it was armed for,
+        // then queue the next one behind the youngest
+        const unsigned long long oldest = w.seq - unsigned(w.armed) + 1;
+        if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < oldest) continue;
+        w.armed -= 1;
+        MPA_HSTAMP('D', r, oldest);
         check_task(r, tasks_[size_t(r - 1)], size_t(w.box->msg_bytes), size_t(w.box->reply_bytes));
         progress = true;
-        if (armable(r)) arm(r);
+        if (armable(r)) arm_up(r);
         continue;
       }
       const unsigned long long db = __atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE);
       if (db == w.seq) continue;
+      MPA_HSTAMP('B', r, db);
       if (db != w.seq + 1) fail(MPA_ERROR, "mailbox protocol: worker %lld doorbell %llu after %llu", (long long)r, db, w.seq);
       if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) != w.seq)
         fail(MPA_ERROR, "mailbox protocol: worker %lld posted while busy", (long long)r);
@@ -69,7 +73,7 @@ void HipComm::serve() {
         while (std::chrono::duration<double, std::micro>(Clock::now() - g0).count() < 2.0) {
           for (int64_t r = 1; r <= nworkers_; ++r) {
             HipWorker& w = w_[size_t(r - 1)];
-            if (!w.here || !w.path_known || w.armed || std::find(fresh.begin(), fresh.end(), r) != fresh.end()) continue;
+            if (!w.here || !w.path_known || w.armed > 0 || std::find(fresh.begin(), fresh.end(), r) != fresh.end()) continue;
             const unsigned long long db = __atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE);
             if (db != w.seq + 1 || __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) != w.seq) continue;
             w.seq = db;
@@ -83,7 +87,7 @@ void HipComm::serve() {
           int postable = 0;  // workers here that could still be posted (not busy, not armed)
           for (int64_t r = 1; r <= nworkers_; ++r) {
             const HipWorker& w = w_[size_t(r - 1)];
-            postable += w.here && w.path_known && !w.armed &&
+            postable += w.here && w.path_known && w.armed == 0 &&
                         (std::find(fresh.begin(), fresh.end(), r) != fresh.end() ||
                          __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) == w.seq);
           }
@@ -94,6 +98,7 @@ void HipComm::serve() {
       }
       if (timing_) reap_timing(false);
       launch_tasks(fresh, /*staged=*/true);
+      MPA_HSTAMP('T', fresh.front(), w_[size_t(fresh.front() - 1)].seq);
       idle = PoliteSpin{};
       idle.yield_cold = true;
       idle.hot_ns = kServerHotSpinNs;
@@ -142,11 +147,13 @@ void HipComm::arm(int64_t rank) {
   HipWorker& w = w_[size_t(rank - 1)];
   const TaskSpec& ts = tasks_[size_t(rank - 1)];
   const unsigned long long s = w.seq + 1;
-  w.arm_sbase = w.lsqb_sbase;
-  w.arm_tbase = w.lsqb_tbase;
-  w.arm_fsbase = w.lsqf_sbase;
-  w.arm_ftbase = w.lsqf_tbase;
+  const int par = int(s & 1);
+  w.arm_sbase[par] = w.lsqb_sbase;
+  w.arm_tbase[par] = w.lsqb_tbase;
+  w.arm_fsbase[par] = w.lsqf_sbase;
+  w.arm_ftbase[par] = w.lsqf_tbase;
   w.seq = s;
+  unsigned long long* cancel = w.cancel_dev + par;
   w.sl = task_msg_bytes(ts);
   w.rl = w.sl * (ts.kind == MPA_TASK_LSQ_BATCH ? 2 : 1);
   w.x = w.xslot;
@@ -159,21 +166,23 @@ void HipComm::arm(int64_t rank) {
   const int64_t sleep_ns = delay - deadline_lead_ns_;
   const unsigned long long sleep_ticks = sleep_ns > 0 ? (unsigned long long)(double(sleep_ns) * rt_hz_ / 1e9) : 0ull;
   if (sleep_ticks) n_sleeps_ += 1;
-  if (arm_wave_) HIPCHECK(launch_door_wait(own_door(w), s, spin_ticks(), err_dev_, w.cancel_dev, sleep_ticks, st));
+  if (arm_wave_) HIPCHECK(launch_door_wait(own_door(w), s, spin_ticks(), err_dev_, cancel, sleep_ticks, st));
+  MPA_HSTAMP('W', rank, s);
   double bytes = 0;
   if (ts.kind == MPA_TASK_LSQ) {
     LsqBatch b = build_lsq_batch({rank}, ts.dtype, &bytes, armed_share());
-    b.t[0].go = w.cancel_dev;
+    b.t[0].go = cancel;
     b.t[0].door = door;
     enqueue_lsq(b, ts.dtype, int(ts.cols), st, bytes, rank);
   } else {
     LsqbLaunch b = build_lsqb_batch({rank}, &bytes, armed_share());
-    b.set_go(w.cancel_dev);
+    b.set_go(cancel);
     b.set_door(door);
     enqueue_lsqb(b, st, bytes, rank);
   }
-  w.armed = true;
+  w.armed += 1;
   n_armed_ += 1;
+  MPA_HSTAMP('L', rank, s);
 }
 
 void HipComm::disarm_all() {
@@ -181,37 +190,57 @@ void HipComm::disarm_all() {
   for (int64_t r = 1; r <= nworkers_; ++r) {
     HipWorker& w = w_[size_t(r - 1)];
     if (!w.here || !w.armed) continue;
-    // release the waiting task with the cancel bit unless rank 0 rang meanwhile (its kernel
-    // stores the device word after the shm one): cancel word first, so every workgroup of a
-    // released task finds it; a cancelled task runs but neither writes nor publishes
+    // release the waiting tasks rank 0 has not rung with the cancel bit (its kernel stores the
+    // device word after the shm one): cancel words first, so every workgroup of a released task
+    // finds its own; a cancelled task runs but neither writes nor publishes.  Rank 0 has
+    // harvested everything it rang before it pauses, so the device word holds the shm value.
+    const unsigned long long newest = w.seq, oldest = w.seq - unsigned(w.armed) + 1;
+    const unsigned long long rung = __atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE);
+    const unsigned long long first = std::max(oldest, rung + 1);  // the first task not rung
     bool cancelled = false;
-    if (__atomic_load_n(&w.box->doorbell, __ATOMIC_ACQUIRE) < w.seq) {
-      __atomic_store_n(w.cancel_host, w.seq, __ATOMIC_SEQ_CST);
-      cancelled = door_cas(w, w.seq - 1, w.seq | kCancelBit);
+    if (first <= newest) {
+      for (unsigned long long s = first; s <= newest; ++s) __atomic_store_n(w.cancel_host + (s & 1), s, __ATOMIC_SEQ_CST);
+      cancelled = door_cas(w, first - 1, newest | kCancelBit);
     }
     (void)hipStreamSynchronize(w.stream);
-    if (cancelled) (void)door_cas(w, w.seq | kCancelBit, w.seq - 1);  // back to "not rung"
+    if (cancelled) (void)door_cas(w, newest | kCancelBit, first - 1);  // back to "not rung"
     __atomic_store_n(w.cancel_host, 0ull, __ATOMIC_SEQ_CST);
-    if (__atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE) < w.seq) {  // it did not run
-      w.seq -= 1;
-      w.lsqb_sbase = w.arm_sbase;
-      w.lsqb_tbase = w.arm_tbase;
-      w.lsqf_sbase = w.arm_fsbase;
-      w.lsqf_tbase = w.arm_ftbase;
-      void_timing(r);
+    __atomic_store_n(w.cancel_host + 1, 0ull, __ATOMIC_SEQ_CST);
+    // the tasks that did not run: the next serve() session arms them again from the counter
+    // bases the first of them started from
+    const unsigned long long ran = __atomic_load_n(w.flag_host, __ATOMIC_ACQUIRE);
+    if (ran < newest) {
+      const int par = int((ran + 1) & 1);
+      w.lsqb_sbase = w.arm_sbase[par];
+      w.lsqb_tbase = w.arm_tbase[par];
+      w.lsqf_sbase = w.arm_fsbase[par];
+      w.lsqf_tbase = w.arm_ftbase[par];
+      for (unsigned long long s = ran + 1; s <= newest; ++s) void_timing(r);
+      w.seq = ran;
     }
-    w.armed = false;
+    w.armed = 0;
   }
+}
+
+int HipComm::arm_depth(int64_t rank) const {
+  if (arm_depth_env_) return arm_depth_env_;
+  return w_[size_t(rank - 1)].box->coord_dev != dev_ ? 2 : 1;
+}
+
+void HipComm::arm_up(int64_t rank) {
+  const int d = arm_depth(rank);
+  while (w_[size_t(rank - 1)].armed < d) arm(rank);
 }
 
 // the worker's device doorbell := desired if it holds expect (a kernel on a launch stream:
 // the word is this GPU's fine-grained memory, which rank 0 stores over xGMI); true if it did
 bool HipComm::door_cas(const HipWorker& w, unsigned long long expect, unsigned long long desired) {
   hipStream_t s = launch_stream(0);
-  __atomic_store_n(&cancel_[nworkers_], ~0ull, __ATOMIC_SEQ_CST);  // scratch: the word's old value
-  HIPCHECK(launch_door_cas(own_door(w), expect, desired, &cancel_[nworkers_], s));
+  unsigned long long* scratch = &cancel_[2 * nworkers_];
+  __atomic_store_n(scratch, ~0ull, __ATOMIC_SEQ_CST);  // the word's old value
+  HIPCHECK(launch_door_cas(own_door(w), expect, desired, scratch, s));
   HIPCHECK(hipStreamSynchronize(s));
-  return __atomic_load_n(&cancel_[nworkers_], __ATOMIC_ACQUIRE) == expect;
+  return __atomic_load_n(scratch, __ATOMIC_ACQUIRE) == expect;
 }
 
 void* HipComm::ipc_alloc(size_t bytes, char* handle, volatile uint32_t* state) {

@@ -156,15 +156,16 @@ struct HipWorker {
   uint8_t* peer_msg = nullptr;
   uint8_t* reply_inbox = nullptr;
   uint8_t* peer_reply = nullptr;
-  // server, pre-armed task (serve()): armed = task `seq` is queued behind its doorbell;
-  // cancel word (host-pinned, device view) of the armed task; counter bases to restore
-  // if cancelled
-  bool armed = false;
+  // server, pre-armed tasks (serve()): armed = how many tasks, `seq - armed + 1` .. `seq`, are
+  // queued behind their doorbells (at most arm_depth_); two cancel words (host-pinned, device
+  // view), task s using word s & 1; the counter bases each armed task started from (by s & 1),
+  // restored if it is cancelled
+  int armed = 0;
   unsigned long long* cancel_host = nullptr;
   unsigned long long* cancel_dev = nullptr;
   // coordinator, launch-ahead: the next post / harvest of this worker is already enqueued
   bool preposted = false, preharvest = false;
-  uint32_t arm_sbase = 0, arm_tbase = 0, arm_fsbase = 0, arm_ftbase = 0;
+  uint32_t arm_sbase[2] = {0, 0}, arm_tbase[2] = {0, 0}, arm_fsbase[2] = {0, 0}, arm_ftbase[2] = {0, 0};
   int64_t tslot = -1;  // task trace (mpa_comm_set_trace): the current task's entry, -1 none
 };
 
@@ -243,8 +244,14 @@ struct HostProfScope {
   }
 };
 #define MPA_HPROF(key) ::mpa::HostProfScope hprof_scope_{key}
+// host event stamps (measurement build, MPA_HOST_STAMP=<dir>: <dir>/<pid>.txt at exit, one line per
+// event: kind, two integers, CLOCK_MONOTONIC ns -- the clock rocprofv3's kernel trace reports, so a
+// run's host events line up with its kernels; tools/arm_timeline.py)
+void host_stamp(char kind, int64_t a, int64_t b);
+#define MPA_HSTAMP(kind, a, b) ::mpa::host_stamp(kind, int64_t(a), int64_t(b))
 #else
 #define MPA_HPROF(key) (void)0
+#define MPA_HSTAMP(kind, a, b) (void)0
 #endif
 
 class HipComm final : public Comm {
@@ -409,6 +416,11 @@ class HipComm final : public Comm {
   // reply's writer and the wait is the kernel's own poll of device memory (wait_door).  With
   // several workers the host-launched path batches a flush's tasks into one launch.
   bool armable(int64_t rank) const;
+  // how many tasks of an armable worker stay queued behind their doorbells: 2 on a GPU that rank 0
+  // does not use (the node's placement), so the task of the epoch after next is enqueued while
+  // this one runs and the last worker to finish an epoch starts the next one from its doorbell,
+  // not from this thread's re-arm; 1 on rank 0's GPU (MPA_ARM_DEPTH=1 / 2 overrides)
+  int arm_depth(int64_t rank) const;
   // local workers that serve() arms: each armed launch gets its share of the launch grid
   int armed_share() const {
     int k = 0;
@@ -424,6 +436,8 @@ class HipComm final : public Comm {
 
   // launch task seq+1 of `rank` on its stream, behind a wait for the device doorbell
   void arm(int64_t rank);
+  // arm until arm_depth(rank) tasks are queued
+  void arm_up(int64_t rank);
 
   // release every waiting armed task: one whose doorbell rank 0 has not rung is cancelled
   // (cancel word := its seq, then device doorbell := seq | kCancelBit to release the wait;
@@ -945,6 +959,7 @@ class HipComm final : public Comm {
   }
   bool debug_ = false;
   int arm_mode_ = 0;
+  int arm_depth_env_ = 0;  // MPA_ARM_DEPTH (0: arm_depth()'s default)
   bool arm_wave_ = true;  // MPA_ARM_WAIT: an armed task waits behind a one-wave door_wait_kernel
   bool arm_force_ = false;  // MPA_ARM_WAIT_FORCE=1 (measurement build): in-kernel waits on rank 0's GPU too
   bool batch_gather_ = true;  // MPA_GATHER=0: a server launches whatever one doorbell scan found

@@ -26,9 +26,52 @@
 // (profiles/r01_hw_queues.txt), which would let one straggler hold back another worker.
 #include "hip_transport.hpp"
 
+#include <time.h>
+#include <unistd.h>
+
 namespace mpa {
 #if MPA_MEASURE
 HostProf g_hprof;
+
+namespace {
+struct HostStamp {
+  char kind;
+  int64_t a, b;
+  int64_t t;
+};
+constexpr size_t kHostStamps = size_t(1) << 20;
+std::vector<HostStamp>* g_hstamp = nullptr;
+std::atomic<size_t> g_hstamp_n{0};
+const char* g_hstamp_dir = nullptr;
+void dump_host_stamps() {
+  if (!g_hstamp) return;
+  char path[512];
+  std::snprintf(path, sizeof path, "%s/%d.txt", g_hstamp_dir, int(getpid()));
+  if (FILE* f = std::fopen(path, "w")) {
+    const size_t n = std::min(g_hstamp_n.load(), kHostStamps);
+    for (size_t k = 0; k < n; ++k) {
+      const HostStamp& h = (*g_hstamp)[k];
+      std::fprintf(f, "%c %lld %lld %lld\n", h.kind, (long long)h.a, (long long)h.b, (long long)h.t);
+    }
+    std::fclose(f);
+  }
+}
+}  // namespace
+
+void host_stamp(char kind, int64_t a, int64_t b) {
+  static const bool on = [] {
+    g_hstamp_dir = std::getenv("MPA_HOST_STAMP");
+    if (!g_hstamp_dir || !*g_hstamp_dir) return false;
+    g_hstamp = new std::vector<HostStamp>(kHostStamps);
+    std::atexit(dump_host_stamps);
+    return true;
+  }();
+  if (!on) return;
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  const size_t k = g_hstamp_n.fetch_add(1, std::memory_order_relaxed);
+  if (k < kHostStamps) (*g_hstamp)[k] = {kind, a, b, int64_t(ts.tv_sec) * 1000000000 + ts.tv_nsec};
+}
 #endif
 
 // rank 0 waits for remote completions of a launched-ahead epoch with one wait_words_kernel
@@ -54,9 +97,10 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   std::memset(flags_, 0, sizeof(unsigned long long) * size_t(n + 1));
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&err_), 64, hipHostMallocCoherent | hipHostMallocMapped));
   std::memset(err_, 0, 64);
-  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&cancel_), sizeof(unsigned long long) * size_t(n + 1),
+  // two cancel words per worker (armed tasks s and s + 1), then the door_cas scratch word
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&cancel_), sizeof(unsigned long long) * size_t(2 * n + 1),
                          hipHostMallocCoherent | hipHostMallocMapped));
-  std::memset(cancel_, 0, sizeof(unsigned long long) * size_t(n + 1));
+  std::memset(cancel_, 0, sizeof(unsigned long long) * size_t(2 * n + 1));
   xgmi_ = !env_off("MPA_XGMI");
   done_dev_ = !env_off("MPA_DONE_DEV");
   // per-task tree counters, then the doorbell ticket and the fused-tail counter
@@ -83,8 +127,8 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
       // the message slot, then the worker's device doorbell word (device-armed tasks wait on it)
       w.xslot = static_cast<uint8_t*>(ipc_alloc(door_off() + 256, w.box->msg_handle, &w.box->msg_ipc));
       HIPCHECK(hipMemset(w.xslot + door_off(), 0, 256));
-      w.cancel_host = &cancel_[r - 1];
-      w.cancel_dev = &cancel_[r - 1];
+      w.cancel_host = &cancel_[2 * (r - 1)];
+      w.cancel_dev = &cancel_[2 * (r - 1)];
     } else if (w.remote) {
       w.flag_host = &w.box->done;
       w.box->coord_dev = dev_;
@@ -138,6 +182,8 @@ HipComm::HipComm(int64_t n, const int* devices, const int* placement, int my_ran
   // where a process serves one worker
   const char* arm = std::getenv("MPA_ARM");
   arm_mode_ = arm && *arm == '0' ? 0 : arm && *arm == '1' ? 1 : 2;
+  const char* ad = std::getenv("MPA_ARM_DEPTH");
+  arm_depth_env_ = ad && (*ad == '1' || *ad == '2') ? *ad - '0' : 0;
   // injected straggler delays: the host timer (default) or a sleep kernel ahead of the task on
   // an unshared worker stream (MPA_DELAY=device); the launch overhead taken out of each sleep
   const char* dl = std::getenv("MPA_DELAY");
@@ -326,7 +372,10 @@ int64_t HipComm::waitany(int64_t n, const int64_t* ranks, const uint8_t* live) {
   PoliteSpin poll;
   for (uint64_t spins = 0;; ++spins) {
     for (int64_t i = 0; i < n; ++i)
-      if (live[i] && done(ranks[i])) return i;
+      if (live[i] && done(ranks[i])) {
+        MPA_HSTAMP('R', ranks[i], w_[size_t(ranks[i] - 1)].seq);
+        return i;
+      }
     if ((spins & 0xFFF) == 0xFFF) watchdog(t0);
     poll();
   }
@@ -838,6 +887,7 @@ void HipComm::maybe_ahead() {
     tail_pending_ = true;
   }
   launch_local(posted);
+  MPA_HSTAMP('A', posted.front(), w_[size_t(posted.front() - 1)].seq);
   if (tail_next_) fail(MPA_ERROR, "fused tail: no least-squares launch took it");
   for (int64_t rank : posted) {
     HipWorker& w = w_[size_t(rank - 1)];

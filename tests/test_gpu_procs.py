@@ -45,13 +45,18 @@ def test_lsq_two_processes_hip(built):
     _run(dist_worker.lsq_dist, 2, [0, 1, 1, 1])
 
 
-def test_lsq_two_processes_prearmed(built, monkeypatch):
-    """Workers 2-4 on rank 1: 2 and 3 pre-armed (no delays; MPA_ARM=1, pre-arming is
-    opt-in), 4 delayed (host-launched); two serve sessions around a pause."""
+# MPA_ARM_DEPTH=2: two tasks of each armed worker queued behind their doorbells (the default on a GPU
+# rank 0 does not use, i.e. the node's; forced here, where every rank shares GPU 0)
+@pytest.mark.parametrize("depth", ["1", "2"])
+def test_lsq_two_processes_prearmed(built, monkeypatch, depth):
+    """Workers 2-4 on rank 1 pre-armed (MPA_ARM=1: every eligible worker, 4 with a delay schedule
+    slept in its doorbell wait); two serve sessions around a pause, whose disarm cancels the
+    queued tasks rank 0 never rang (one or two per worker) and re-arms them in the next session."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     monkeypatch.setenv("MPA_ARM", "1")  # the spawned ranks inherit it
+    monkeypatch.setenv("MPA_ARM_DEPTH", depth)
     _run(dist_worker.lsq_dist_armed, 2, [0, 1, 1, 1], [4])
 
 
@@ -73,15 +78,17 @@ def test_lsqb_two_processes(built, monkeypatch, arm, cols):
 # (door_wait_kernel), so seven waiting tasks hold seven waves, not seven launch grids
 # (round 3's in-kernel wait timed out here, profiles/r03_rehearsal_n248.txt).
 
-def test_lsq_descent_eight_processes_armed(built):
+@pytest.mark.parametrize("depth", ["1", "2"])
+def test_lsq_descent_eight_processes_armed(built, depth):
     """BASELINE c2's N = 8 placement (rank 0 coordinates and serves worker 1, ranks 1-7 one
-    worker each, device-armed by default): the native loop's iterate, replies and messages
-    bitwise equal to the one-process Python loop on the same shards, and every server
-    armed its tasks."""
+    worker each, device-armed by default, one or two tasks deep): the native loop's iterate,
+    replies and messages bitwise equal to the one-process Python loop on the same shards, and
+    every server armed its tasks."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _run(dist_worker.lsq_descent_dist, 8, list(range(8)), {"MPA_TEST_EXPECT_ARMED": "1"}, timeout=240)
+    _run(dist_worker.lsq_descent_dist, 8, list(range(8)), {"MPA_TEST_EXPECT_ARMED": "1", "MPA_ARM_DEPTH": depth},
+         timeout=240)
 
 
 def test_lsq_descent_eight_processes_host_launched(built):
@@ -92,14 +99,16 @@ def test_lsq_descent_eight_processes_host_launched(built):
     _run(dist_worker.lsq_descent_dist, 8, list(range(8)), {"MPA_ARM": "0", "MPA_TEST_EXPECT_ARMED": "0"}, timeout=240)
 
 
-def test_lsqb_eight_processes_armed(built, monkeypatch):
+@pytest.mark.parametrize("depth", ["1", "2"])
+def test_lsqb_eight_processes_armed(built, monkeypatch, depth):
     """BASELINE c5's N = 8 placement: the batched 64-iterate task at 2048 columns (lsqp4's
-    FULL form) in eight processes, every server device-armed, every G against the fp64
-    oracle at 1e-5."""
+    FULL form) in eight processes, every server device-armed (one or two tasks deep), every G
+    against the fp64 oracle at 1e-5."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     monkeypatch.delenv("MPA_ARM", raising=False)
+    monkeypatch.setenv("MPA_ARM_DEPTH", depth)
     _run(dist_worker.lsqb_dist, 8, list(range(8)), 2048, True, timeout=240)
 
 
@@ -134,8 +143,9 @@ def test_sched_eight_processes(built, config, epoch0):
     _run(dist_worker.lsq_sched_dist, 8, list(range(8)), config, epoch0, timeout=240)
 
 
-@pytest.mark.parametrize("config,epoch0", [("c3", 0), ("c4", 0), ("c4", 1000), ("c5", 0)])
-def test_native_kofn_descent_eight_processes(built, config, epoch0):
+@pytest.mark.parametrize("config,epoch0,depth", [("c3", 0, "1"), ("c4", 0, "1"), ("c4", 1000, "1"), ("c5", 0, "1"),
+                                                 ("c3", 0, "2"), ("c5", 0, "2")])
+def test_native_kofn_descent_eight_processes(built, monkeypatch, config, epoch0, depth):
     """The native k-of-n coordinator loop across processes -- bench.py's rank 0 at N > 1 for
     c3 (fp32, nwait 6 of 8), c4 (fp64, first_plus(5), stale weight 0.5, epoch0 0 and 1000) and
     c5 (bf16 batched, nwait 7) -- in the node's placement on GPU 0, ungated: the final iterate
@@ -144,19 +154,23 @@ def test_native_kofn_descent_eight_processes(built, config, epoch0):
     re-dispatch launched at once on rank 0 of the node's placement and held into the next launch
     where rank 0 serves a second worker (c5)
     (dist_worker.descent_kofn_dist; one process: tests/test_gpu.py
-    test_native_k_of_n_prearmed_with_stragglers)."""
+    test_native_k_of_n_prearmed_with_stragglers); armed one or two tasks deep."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("MPA_ARM_DEPTH", depth)
     world = max(dist_worker.KOFN_CONFIGS[config]["placement"]) + 1
     _run(dist_worker.descent_kofn_dist, world, config, epoch0, timeout=240)
 
 
-def test_armed_wait_timeout_cancels_the_task(built):
+@pytest.mark.parametrize("depth", ["1", "2"])
+def test_armed_wait_timeout_cancels_the_task(built, monkeypatch, depth):
     """a device-armed task whose doorbell wait times out is cancelled (the one-wave
     door_wait_kernel stores the task's seq into its go word): no reply, no `done`, the error
-    reported by the server's serve()."""
+    reported by the server's serve(); at depth 2 the task queued behind it is cancelled by the
+    disarm."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("MPA_ARM_DEPTH", depth)
     _run(dist_worker.armed_timeout_dist, 2, timeout=120)
