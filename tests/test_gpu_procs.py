@@ -144,7 +144,7 @@ def test_sched_eight_processes(built, config, epoch0):
 
 
 @pytest.mark.parametrize("config,epoch0,depth", [("c3", 0, "1"), ("c4", 0, "1"), ("c4", 1000, "1"), ("c5", 0, "1"),
-                                                 ("c3", 0, "2"), ("c5", 0, "2")])
+                                                 ("c3", 0, "2"), ("c4", 1000, "2"), ("c5", 0, "2")])
 def test_native_kofn_descent_eight_processes(built, monkeypatch, config, epoch0, depth):
     """The native k-of-n coordinator loop across processes -- bench.py's rank 0 at N > 1 for
     c3 (fp32, nwait 6 of 8), c4 (fp64, first_plus(5), stale weight 0.5, epoch0 0 and 1000) and
