@@ -399,13 +399,13 @@ class HipComm final : public Comm {
   void on_delays_changed(int64_t rank) override;
 
   // ---- worker process: watch the doorbells of the workers served here ----
-  // Least-squares workers without a delay schedule whose messages arrive in this GPU's slot
-  // are DEVICE-ARMED (armable): their next task is already launched and waits in-kernel for
-  // the worker's device doorbell, which rank 0 stores over xGMI right after the message.
-  // Other workers (the reference's test programs, injected delays, the host mailbox) are
-  // launched by this thread when it sees their shared-memory doorbell.  serve() returns at
-  // pause / shutdown after disarming: waiting tasks are released with kCancelBit and return
-  // without writing or publishing.
+  // Least-squares workers whose messages arrive in this GPU's slot are DEVICE-ARMED
+  // (armable): their next task (two, arm_depth) is already queued behind a one-wave wait for
+  // the worker's device doorbell, which rank 0 stores over xGMI right after the message (a
+  // delayed worker's wait then sleeps its delay).  Other workers (the reference's test
+  // programs, the host mailbox) are launched by this thread when it sees their shared-memory
+  // doorbell.  serve() returns at pause / shutdown after disarming: the waiting tasks rank 0
+  // has not rung are released with kCancelBit and return without writing or publishing.
   void serve();
 
   // ---- device-armed tasks (server) ----
