@@ -282,6 +282,7 @@ struct LsqpBatch {
   int ntasks;
   int pfd;  // L2 prefetch lead over the LDS-DMA, in blocks (0: none); MPA_LSQP_PF.  lsqc: phase-1 lookahead (1, 2)
   int dbg;  // measurement build only (MPA_LSQP_DBG): 1 no DMA, 2 no compute, 8/16/32 no phase 1 / reduce / phase 2
+  int xred;  // lsqp4: G over the row groups in a second launch (set by launch_lsqp4; MPA_LSQP4_XRED=0: in-kernel tree)
   int grp0[kMaxLsqTasks + 1];  // lsqp/lsqp4: pairs before task t; lsqc: workgroups before task t
   LsqpTask t[kMaxLsqTasks];
   // column pairs (lsqc_kernel.hip) only

@@ -43,6 +43,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "device_common.hpp"
@@ -98,7 +99,8 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 // MPA_LSQP4_PROBE (timing-probe builds only, wrong results: make BUILD=... EXTRA=-DMPA_LSQP4_PROBE=n,
 // profiles/r03_c5_probes.txt): 1 no strip DMAs in the block loop, 2 no cross-wave exchange /
 // barrier in the reduce, 4 no phase-1 MFMAs, 8 half the phase-2 LDS reads (r04_c5_pipelined.txt),
-// 16 no L2 prefetch (r06: 1 | 16 = the loop with no memory traffic but B, profiles/r06_c5_prefetch_cu.txt)
+// 16 no L2 prefetch (r06: 1 | 16 = the loop with no memory traffic but B, profiles/r06_c5_prefetch_cu.txt),
+// 32 no G tree (every wave stores its partial and goes to the publish: what the tree costs a launch)
 #ifndef MPA_LSQP4_PROBE
 #define MPA_LSQP4_PROBE 0
 #endif
@@ -692,9 +694,13 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) st_wt(slab + size_t(q) * qstride + (t * NCT + ct) * 64 + lane, G[t][ct]);
+    if (batch.xred) return;  // lsqp4_reduce_kernel sums the partials, writes G and publishes
     unsigned idx = unsigned(q), count = unsigned(ng), stride = 1;
     int lvl_off = 0, lvl_cap = (kLsqpMaxGroups + PF - 1) / PF;
     for (;;) {
+#if MPA_LSQP4_PROBE & 32
+      break;
+#endif
       drain_vm();
       const unsigned first = (idx / PF) * PF;
       const unsigned gsize = count - first < unsigned(PF) ? count - first : unsigned(PF);
@@ -764,6 +770,124 @@ __global__ void __launch_bounds__(QT, 1) lsqp4_kernel(LsqpBatch batch) {
   }
 }
 
+// ---- G over the row groups as a second launch, for a launch of ONE task (round 6, the default;
+// MPA_LSQP4_XRED=0 keeps the in-kernel tree above).  In the tree the last arriver of a group sums
+// it, so at the upper levels a handful of waves move 256 KiB each while the rest of the chip idles:
+// a lone task's four levels took 105 us of its 1.04 ms launch (c5n8: the node's per-GPU launch at
+// N = 8, and every lone stale re-dispatch; profiles/r06_c5_xred.txt).  A launch of several tasks
+// keeps the tree: there each task completes on its own, as soon as its tree is summed, where a
+// second launch would hold every task's completion until the slowest task's row groups finish
+// (the native k-of-n loop's c5 case: the small local worker's latency 0.1 -> 1.8 ms).  Here every (task, half,
+// wave) slice is split over 16 workgroups, one thread per 16-B element of G, and each thread sums
+// that element's partials over the row groups in the tree's own order -- groups of PF in member
+// order, level by level, the short last group of a level passed up as it is -- with a stack of
+// one pending sum per level, so G is bitwise what the tree gives.  The task's last workgroup
+// publishes.
+constexpr int kRedThreads = 256;
+constexpr int kRedChunks = (2 * NCT * 64) / kRedThreads;  // workgroups per (half, wave) slice
+constexpr int kRedPerTask = 2 * QW * kRedChunks;           // workgroups per task
+constexpr int kRedLevels = 6;                              // PF^5 >= kLsqpMaxGroups
+constexpr int kRedBatch = 16;                              // partial loads in flight per thread
+static_assert(kRedChunks * kRedThreads == 2 * NCT * 64, "whole slices");
+static_assert(PF * PF * PF * PF * PF >= kLsqpMaxGroups, "levels");
+
+__global__ void __launch_bounds__(kRedThreads) lsqp4_reduce_kernel(LsqpBatch batch) {
+  const int ti = int(blockIdx.x) / kRedPerTask;
+  if (ti >= batch.ntasks) return;
+  const LsqpTask& a = batch.t[ti];
+  const int ng = batch.grp0[ti + 1] - batch.grp0[ti];
+  if (ng <= 1) return;  // lsqp4 stored and published that task itself
+  const int r = int(blockIdx.x) % kRedPerTask;
+  const int h = r / (QW * kRedChunks), w = (r / kRedChunks) % QW, chunk = r % kRedChunks;
+  const int e = chunk * kRedThreads + int(threadIdx.x);  // element of the slice: tile j, lane
+  const int j = e >> 6, lane = e & 63, t = j / NCT, ct = j % NCT, i = lane & 15, g = lane >> 4;
+  const int cols = a.cols, c0 = w * QKW;
+  const int nks = cols > c0 ? ((cols - c0) < QKW ? (cols - c0) : QKW) / 32 : 0;
+  const int col = c0 + 16 * ct + i;
+  const bool valid = ct < 2 * nks && col < cols;
+  __shared__ int s_cx;
+  if (threadIdx.x < 64) {  // one wave: the go word (host memory) and, in-kernel armed, a timed-out wait
+    bool cx = disarmed(a.go, a.seq);
+    if (a.door && (__hip_atomic_load(batch.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 64u)) cx = true;
+    if (threadIdx.x == 0) s_cx = cx;
+  }
+  if (valid) {
+    const size_t wslab = size_t(2 * NCT) * 64, qstride = size_t(QW) * wslab;
+    const f32x4* __restrict__ src =
+        static_cast<const f32x4*>(a.slab) + (size_t(h) * kLsqpMaxGroups * QW + w) * wslab + e;
+    f32x4 lv[kRedLevels];
+    int n[kRedLevels];  // members summed at each level (the same in every thread)
+#pragma unroll
+    for (int l = 0; l < kRedLevels; ++l) n[l] = 0;
+    // add x as the next member at level l0; a group of PF members goes up as one
+    auto push = [&](int l0, f32x4 x) __attribute__((always_inline)) {
+#pragma unroll
+      for (int l = 0; l < kRedLevels; ++l) {
+        if (l < l0) continue;
+        if (n[l] == 0) lv[l] = x;
+        else lv[l] = lv[l] + x;
+        if (++n[l] < PF) return;
+        n[l] = 0;
+        x = lv[l];
+      }
+    };
+    for (int q0 = 0; q0 < ng; q0 += kRedBatch) {
+      f32x4 v[kRedBatch];
+#pragma unroll
+      for (int k = 0; k < kRedBatch; ++k) v[k] = ld_wt(src + size_t(q0 + k < ng ? q0 + k : q0) * qstride);
+#pragma unroll
+      for (int k = 0; k < kRedBatch; ++k)
+        if (q0 + k < ng) push(0, v[k]);
+    }
+    // the short last group of each level goes up as the last member of the next; the lowest
+    // level with members and none above is the root
+    f32x4 res = lv[0];
+    bool done = false;
+#pragma unroll
+    for (int l = 0; l < kRedLevels; ++l) {
+      bool above = false;
+#pragma unroll
+      for (int m = l + 1; m < kRedLevels; ++m) above = above || n[m] > 0;
+      if (!done && n[l] > 0) {
+        if (above) {
+          n[l] = 0;
+          push(l + 1, lv[l]);
+        } else {
+          res = lv[l];
+          done = true;
+        }
+      }
+    }
+    __syncthreads();  // s_cx
+    if (!s_cx) *reinterpret_cast<f32x4*>(static_cast<float*>(a.out) + size_t(col) * K + PH * h + 16 * t + 4 * g) = res;
+  } else {
+    __syncthreads();
+  }
+  drain_vm();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    uint32_t* c = &a.ctr[2 * 8 * kLsqpCtrPerSlice];  // the slice-completion counter the tree path uses
+    const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == unsigned(kRedPerTask)) {
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (!s_cx) {
+        publish_task(a.flag, a.seq, a.pub_local);
+        publish_peer(a.flag2, a.seq);
+      }
+    }
+  }
+}
+
+static bool xred_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MPA_LSQP4_XRED");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 }  // namespace
 
 #if MPA_MEASURE
@@ -787,17 +911,24 @@ void lsqp4_clock_dump() {
 }
 #endif
 
-hipError_t launch_lsqp4(const LsqpBatch& a, hipStream_t s) {
-  const int pairs = a.grp0[a.ntasks];
+hipError_t launch_lsqp4(const LsqpBatch& a0, hipStream_t s) {
+  const int pairs = a0.grp0[a0.ntasks];
   if (pairs <= 0) return hipErrorInvalidValue;
   const int grid = (pairs + 7) / 8 * 16;
-  bool full = true;
-  for (int t = 0; t < a.ntasks; ++t) full = full && a.t[t].cols == kLsqpMaxCols && a.t[t].rows % PRB == 0;
+  LsqpBatch a = a0;
+  bool full = true, multi = false;
+  for (int t = 0; t < a.ntasks; ++t) {
+    full = full && a.t[t].cols == kLsqpMaxCols && a.t[t].rows % PRB == 0;
+    multi = multi || a.grp0[t + 1] - a.grp0[t] > 1;
+    if (a.grp0[t + 1] - a.grp0[t] > kLsqpMaxGroups) return hipErrorInvalidValue;
+  }
+  a.xred = xred_enabled() && multi && a.ntasks == 1;
   const bool armed = batch_armed(a);
   if (armed && full) hipLaunchKernelGGL((lsqp4_kernel<true, true>), dim3(grid), dim3(QT), 0, s, a);
   else if (armed) hipLaunchKernelGGL((lsqp4_kernel<true, false>), dim3(grid), dim3(QT), 0, s, a);
   else if (full) hipLaunchKernelGGL((lsqp4_kernel<false, true>), dim3(grid), dim3(QT), 0, s, a);
   else hipLaunchKernelGGL((lsqp4_kernel<false, false>), dim3(grid), dim3(QT), 0, s, a);
+  if (a.xred) hipLaunchKernelGGL(lsqp4_reduce_kernel, dim3(a.ntasks * kRedPerTask), dim3(kRedThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -276,4 +276,39 @@ for rows, cols, n, seed in T._VARIANT_CASES:
     outs.append(out)
 np.savez(sys.argv[2], *outs)
 """
-_VARIANT_CASES = [(4800, 2048, 2, 91), (3001, 2048, 3, 92), (2500, 1312, 2, 93)]
+# lone tasks (the second launch's case) of 128, 128, 63 and 17 row groups (trees of 4, 3 and 3 levels,
+# short last groups at several levels), ragged rows, 1312 and 512 columns (waves with part of a slice
+# or none); and a batch of two tasks, which keeps the in-kernel tree either way
+_VARIANT_CASES = [(4800, 2048, 1, 95), (3001, 1312, 1, 96), (1000, 2048, 1, 97), (272, 512, 1, 98),
+                  (2500, 2048, 2, 99)]
+
+
+def _variant_outputs(tmp_path, tag, env_extra):
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / f"{tag}.npz")
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([sys.executable, "-c", _VARIANT_CHILD, root, out], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    z = np.load(out)
+    return [z[f"arr_{k}"] for k in range(len(_VARIANT_CASES))]
+
+
+def test_lsqp4_second_launch_reduce_matches_tree_bitwise(M, tmp_path):
+    """A lone task's G over the row groups in a second launch (lsqp4_reduce_kernel, the default)
+    against the in-kernel tree (MPA_LSQP4_XRED=0), each in a process of its own: bit for bit on
+    every case -- the reduction keeps the tree's summation order -- and every G within 1e-5 of the
+    fp64 oracle."""
+    import lsq
+    new = _variant_outputs(tmp_path, "xred", {"MPA_LSQP4_XRED": "1"})
+    old = _variant_outputs(tmp_path, "tree", {"MPA_LSQP4_XRED": "0"})
+    for (rows, cols, n, seed), a, b in zip(_VARIANT_CASES, new, old):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (rows, cols, n)
+        A, B, X = _problem(n * rows, cols, seed)
+        for i in range(n):
+            lo, hi = i * rows, (i + 1) * rows - (i if rows % 16 else 0)
+            err = lsq.rel_err(a[i], lsq.batched_shard_gradient(A[lo:hi], B[lo:hi], X, "bf16"))
+            assert err <= TOL, (rows, cols, n, i, err)
