@@ -35,6 +35,8 @@
 //   M_HEAD      (set per launch) the fused head: workgroup 0 runs the epoch step first
 //               (LsqBatch::head); a prologue the other launches must not carry (its mere
 //               presence cost the c2 launch 19 %)
+//   M_ROTATE    grid sweeps with the workgroup's tile rotated by one per sweep (below; c2's
+//               shape, where it measured faster)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -57,7 +59,8 @@ namespace {
 
 using namespace dev;
 
-enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16, M_BLOCKED = 32, M_ARMED = 64, M_HEAD = 128 };
+enum : int { M_CLAMP = 1, M_DPP = 2, M_PREFETCH = 4, M_NT = 8, M_TREE_FENCE = 16, M_BLOCKED = 32, M_ARMED = 64, M_HEAD = 128,
+             M_ROTATE = 256 };
 
 template <typename T, int VPL, int RB, int MODE>
 struct Tile {
@@ -232,7 +235,19 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   }
 
   const int64_t rows = a.rows;
-  int64_t step, base, hi;  // this wave's tiles: base, base + step, ... < hi
+  int64_t step, base, hi;  // this wave's tiles: base, then nxt(), ... while < hi
+  // Grid sweeps (not M_BLOCKED): sweep k covers rows [k step, (k + 1) step), one tile of
+  // kWaves * RB rows per workgroup, workgroup blk taking tile blk of it -- or, M_ROTATE, tile
+  // (blk + k) mod grid.  The rotation moves every workgroup -- and so every XCD, which
+  // round-robin placement gives the workgroups of one residue mod 8 -- across all the sweep's
+  // tile address classes: with tile blk of every sweep, the XCDs of one parity ended their loops
+  // ~12 us (1.8 %) after the other's in every c2 launch, the launch waiting for the slower
+  // (profiles/r06_lsq_rotation.txt: c2 +0.4-1.2 % in 7 of 7 same-box pairs; c3's 128-KiB tiles
+  // -1.3 %, c1 level within its noise, so only c2's shape rotates).  Each wave still sums its own
+  // tiles in sweep order: deterministic, the same in every variant of a shape.
+  int64_t org = 0;
+  int rot = blk;
+  const int grid1 = a.grid;
   if constexpr (MODE & M_BLOCKED) {
     const int64_t tile = int64_t(kWaves) * RB;
     const int64_t per = ((rows + a.grid - 1) / a.grid + tile - 1) / tile * tile;
@@ -245,6 +260,17 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
     base = (int64_t(blk) * kWaves + wave) * RB;
     hi = rows;
   }
+  // the wave's next tile (bases strictly increase, so the first one past hi ends the loop)
+  auto nxt = [&]() -> int64_t {
+    if constexpr ((MODE & M_BLOCKED) || !(MODE & M_ROTATE)) {
+      base += step;
+    } else {
+      org += step;
+      rot = rot + 1 == grid1 ? 0 : rot + 1;
+      base = org + (int64_t(rot) * kWaves + wave) * RB;
+    }
+    return base;
+  };
 
   // Fused head: workgroup 0 runs this epoch's coordinator step; its dispatch copies (the
   // messages the tasks read) are stored write-through, the others' first tile of A is in
@@ -363,24 +389,24 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       t0.load_b(bv, base, rows);
     }
     for (;;) {
-      const int64_t b1 = base + step;
-      if (base >= hi) break;
+      const int64_t b0 = base;
+      if (b0 >= hi) break;
+      const int64_t b1 = nxt();
       if (b1 < hi) {
         t1.load(A, b1, rows, a.lda, lane, vok);
         t1.load_b(bv, b1, rows);
       }
-      t0.compute(bv, base, rows, xr, g);
-      const int64_t b2 = b1 + step;
+      t0.compute(bv, b0, rows, xr, g);
       if (b1 >= hi) break;
+      const int64_t b2 = nxt();
       if (b2 < hi) {
         t0.load(A, b2, rows, a.lda, lane, vok);
         t0.load_b(bv, b2, rows);
       }
       t1.compute(bv, b1, rows, xr, g);
-      base = b2;
     }
   } else if constexpr ((MODE & M_HEAD) != 0) {
-    for (; base < hi; base += step) {
+    for (; base < hi; nxt()) {
       if (!pre) {
         t0.load(A, base, rows, a.lda, lane, vok);
         t0.load_b(bv, base, rows);
@@ -389,7 +415,7 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
       t0.compute(bv, base, rows, xr, g);
     }
   } else {
-    for (; base < hi; base += step) {
+    for (; base < hi; nxt()) {
       Tile<T, VPL, RB, MODE> t;
       t.load(A, base, rows, a.lda, lane, vok);
       t.compute(bv, base, rows, xr, g);
@@ -654,8 +680,9 @@ struct Variant {
 };
 constexpr Variant kC2Variants[] = {
     // shipped: 6.5 TB/s on c2 in the round-1 sweep (profiles/r01_tune_sweep*.jsonl)
-    {go<float, 4, 4, M_CLAMP | M_DPP | M_NT>, 4, "rb4+clamp+dpp+nt"},
+    {go<float, 4, 4, M_CLAMP | M_DPP | M_NT | M_ROTATE>, 4, "rb4+clamp+dpp+nt+rotate"},
 #if MPA_MEASURE
+    {go<float, 4, 4, M_CLAMP | M_DPP | M_NT>, 4, "rb4+clamp+dpp+nt (round 5's, no rotation)"},
     // the tuning space of that sweep (measurement build only: make MEASURE=1)
     {go<float, 4, 4, 0>, 4, "rb4"},
     {go<float, 4, 4, M_CLAMP>, 4, "rb4+clamp"},
@@ -777,6 +804,16 @@ void lsq_stamp_dump() {
                "loop ends p10 %.2f median %.2f last %.2f, last tree root %.2f, last publish %.2f\n", n,
                double(s1 - t0) / 100.0, ends[n / 10], ends[n / 2], ends.back(), double(root - t0) / 100.0,
                double(pub - t0) / 100.0);
+  // by blockIdx % 8 (the XCD under round-robin placement): median and last loop end
+  std::fprintf(stderr, "[mpa lsq stamps] loop ends by workgroup %% 8 (median / last):");
+  for (unsigned x = 0; x < 8; ++x) {
+    std::vector<double> e;
+    for (unsigned b = x; b < n; b += 8) e.push_back(double(wg[b][1] - t0) / 100.0);
+    if (e.empty()) continue;
+    std::sort(e.begin(), e.end());
+    std::fprintf(stderr, " %u: %.1f / %.1f", x, e[e.size() / 2], e.back());
+  }
+  std::fprintf(stderr, "\n");
 }
 #endif
 
