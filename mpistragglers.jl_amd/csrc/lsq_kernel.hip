@@ -238,13 +238,13 @@ __global__ void __launch_bounds__(kThreads) lsq_grad_kernel(LsqBatch batch) {
   int64_t step, base, hi;  // this wave's tiles: base, then nxt(), ... while < hi
   // Grid sweeps (not M_BLOCKED): sweep k covers rows [k step, (k + 1) step), one tile of
   // kWaves * RB rows per workgroup, workgroup blk taking tile blk of it -- or, M_ROTATE, tile
-  // (blk + k) mod grid.  The rotation moves every workgroup -- and so every XCD, which
-  // round-robin placement gives the workgroups of one residue mod 8 -- across all the sweep's
-  // tile address classes: with tile blk of every sweep, the XCDs of one parity ended their loops
-  // ~12 us (1.8 %) after the other's in every c2 launch, the launch waiting for the slower
-  // (profiles/r06_lsq_rotation.txt: c2 +0.4-1.2 % in 7 of 7 same-box pairs; c3's 128-KiB tiles
-  // -1.3 %, c1 level within its noise, so only c2's shape rotates).  Each wave still sums its own
-  // tiles in sweep order: deterministic, the same in every variant of a shape.
+  // (blk + k) mod grid.  Motivated by a split by XCD (round-robin placement gives an XCD the
+  // workgroups of one residue mod 8): the XCDs of one parity ended their loops ~12 us after the
+  // other's in every c2 launch.  The split persists with the rotation (so it is not the tiles'
+  // addresses), but c2 measured +0.4-1.2 % rotated in 7 of 7 same-box pairs; c3's 128-KiB tiles
+  // -1.3 %, its delayed lone tasks -7 %, c1 level: only c2's shape rotates
+  // (profiles/r06_lsq_rotation.txt).  Each wave still sums its own tiles in sweep order:
+  // deterministic, the same in every variant of a shape.
   int64_t org = 0;
   int rot = blk;
   const int grid1 = a.grid;
