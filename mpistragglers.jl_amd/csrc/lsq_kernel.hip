@@ -168,12 +168,21 @@ __device__ __forceinline__ void head_stamp(uint32_t token, int k, bool first) {
 // measurement build (MPA_LSQ_STAMP=1 dumps them): s_memrealtime of the last launch, per workgroup
 // [0] entry and [1] end of its block loop; the launch's last tree root start and last publish
 constexpr int kLsqStampWgs = 1024;
-__device__ unsigned long long g_lsq_wg[kLsqStampWgs][2];
+__device__ unsigned long long g_lsq_wg[kLsqStampWgs][4];  // realtime entry / loop end, shader clock entry / loop end
+__device__ unsigned g_lsq_xcc[kLsqStampWgs];             // the XCC the workgroup ran on (HW_REG_XCC_ID)
 __device__ unsigned long long g_lsq_root, g_lsq_pub;
 __device__ unsigned g_lsq_grid;
 #define MPA_LSQ_WG_STAMP(k) \
   do {                     \
-    if (threadIdx.x == 0 && blockIdx.x < kLsqStampWgs) g_lsq_wg[blockIdx.x][k] = rt_now(); \
+    if (threadIdx.x == 0 && blockIdx.x < kLsqStampWgs) {                                   \
+      g_lsq_wg[blockIdx.x][k] = rt_now();                                                    \
+      g_lsq_wg[blockIdx.x][2 + k] = __builtin_amdgcn_s_memtime();                            \
+      if (k == 0) {                                                                          \
+        unsigned xcc_;                                                                       \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                 \
+        g_lsq_xcc[blockIdx.x] = xcc_ & 0xF;                                                  \
+      }                                                                                      \
+    }                                                                                        \
   } while (0)
 #define MPA_LSQ_MAX_STAMP(v) atomicMax(&(v), rt_now())
 #else
@@ -782,13 +791,15 @@ const char* lsq_variant_name() { return kC2Variants[c2_variant()].name; }
 // workgroup's entry (us): the last entry, the block loops' ends (median, last), the last tree
 // root's start and the last publish
 void lsq_stamp_dump() {
-  static unsigned long long wg[kLsqStampWgs][2];
+  static unsigned long long wg[kLsqStampWgs][4];
+  static unsigned xcc[kLsqStampWgs];
   unsigned long long root = 0, pub = 0;
   unsigned grid = 0;
   if (hipMemcpyFromSymbol(wg, HIP_SYMBOL(g_lsq_wg), sizeof(wg)) != hipSuccess ||
       hipMemcpyFromSymbol(&root, HIP_SYMBOL(g_lsq_root), sizeof(root)) != hipSuccess ||
       hipMemcpyFromSymbol(&pub, HIP_SYMBOL(g_lsq_pub), sizeof(pub)) != hipSuccess ||
-      hipMemcpyFromSymbol(&grid, HIP_SYMBOL(g_lsq_grid), sizeof(grid)) != hipSuccess)
+      hipMemcpyFromSymbol(&grid, HIP_SYMBOL(g_lsq_grid), sizeof(grid)) != hipSuccess ||
+      hipMemcpyFromSymbol(xcc, HIP_SYMBOL(g_lsq_xcc), sizeof(xcc)) != hipSuccess)
     return;
   const unsigned n = grid < unsigned(kLsqStampWgs) ? grid : unsigned(kLsqStampWgs);
   if (!n) return;
@@ -812,6 +823,36 @@ void lsq_stamp_dump() {
     if (e.empty()) continue;
     std::sort(e.begin(), e.end());
     std::fprintf(stderr, " %u: %.1f / %.1f", x, e[e.size() / 2], e.back());
+  }
+  std::fprintf(stderr, "\n");
+  // the shader clock over each workgroup's block loop (s_memtime cycles / s_memrealtime at 100 MHz)
+  std::fprintf(stderr, "[mpa lsq stamps] loop clock GHz by workgroup %% 8 (median):");
+  for (unsigned x = 0; x < 8; ++x) {
+    std::vector<double> c;
+    for (unsigned b = x; b < n; b += 8)
+      if (wg[b][1] > wg[b][0]) c.push_back(double(wg[b][3] - wg[b][2]) / double(wg[b][1] - wg[b][0]) * 0.1);
+    if (c.empty()) continue;
+    std::sort(c.begin(), c.end());
+    std::fprintf(stderr, " %u: %.3f", x, c[c.size() / 2]);
+  }
+  std::fprintf(stderr, "\n");
+  // by the XCC the workgroup actually ran on: how many, loop end median, clock median; and how
+  // many workgroups ran on XCC (blockIdx % 8)
+  unsigned match = 0;
+  for (unsigned b = 0; b < n; ++b) match += xcc[b] == b % 8;
+  std::fprintf(stderr, "[mpa lsq stamps] by XCC (workgroups, loop end median, clock GHz median); %u of %u on XCC blockIdx %% 8:",
+               match, n);
+  for (unsigned x = 0; x < 8; ++x) {
+    std::vector<double> e, c;
+    for (unsigned b = 0; b < n; ++b)
+      if (xcc[b] == x) {
+        e.push_back(double(wg[b][1] - t0) / 100.0);
+        if (wg[b][1] > wg[b][0]) c.push_back(double(wg[b][3] - wg[b][2]) / double(wg[b][1] - wg[b][0]) * 0.1);
+      }
+    if (e.empty()) continue;
+    std::sort(e.begin(), e.end());
+    std::sort(c.begin(), c.end());
+    std::fprintf(stderr, " %u: %zu %.1f %.3f", x, e.size(), e[e.size() / 2], c.empty() ? 0.0 : c[c.size() / 2]);
   }
   std::fprintf(stderr, "\n");
 }
