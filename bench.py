@@ -476,6 +476,13 @@ def run_single(args, cfg):
     nwait = _nwait(M, cfg)
     k = cfg.get("iterates", 1)
     batched = k > 1
+    if os.environ.get("MPA_BENCH_LSQ_GRID"):
+        # measurement knob (grid sweeps on the product library): workgroups per least-squares
+        # launch, mpa_tune("lsq_grid"); the line says so in its workload
+        G = int(os.environ["MPA_BENCH_LSQ_GRID"])
+        if M.lib().mpa_tune(b"lsq_grid", G) != 0:
+            raise SystemExit("mpa_tune lsq_grid %d refused" % G)
+        cfg["desc"] = "lsq_grid %d (MPA_BENCH_LSQ_GRID, not the shipped grid): " % G + cfg["desc"]
     comm = M.DeviceComm(n)
     shards = gen_shards(M, torch, cfg, args.seed, range(1, n + 1))
     torch.cuda.synchronize()
